@@ -1,0 +1,43 @@
+# Builds the MI355X (gfx950) sampling path: librtw.so (C ABI, include/rtw_capi.h),
+# the rtw_cli driver (mirrors the reference's main.rs), and the test-only oracle.
+# Everything f64 is compiled with -ffp-contract=off (no FMA contraction): parity
+# with the reference's generic x86-64 release build depends on it.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+PKG := raytracing_in_a_weekend_rust_amd
+SRC := $(PKG)/csrc
+OUT := $(PKG)/_lib
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+            -Wall -Iinclude -I$(SRC) -I$(SRC)/host
+CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
+            -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
+
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle
+
+$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+	@mkdir -p $(OUT)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
+
+$(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN' -lpthread
+
+oracle:
+	$(MAKE) -C oracle
+
+asm: $(SRC)/rtw_render.hip
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/rtw_render.s $<
+
+clean:
+	rm -rf $(OUT) build
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle asm clean

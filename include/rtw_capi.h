@@ -1,0 +1,179 @@
+/*
+ * rtw_capi.h -- C ABI of the MI355X-native sampling path (librtw.so).
+ *
+ * Drop-in boundary for NicoElbers/Raytracing_in_a_weekend_rust's per-pixel hot
+ * path. The reference has no FFI; its swappable seam is
+ *   Camera::threaded_render(cam: &Arc<Camera>, world: &Arc<dyn Hittable>,
+ *                           samples_sqrt: usize) -> Result<(), Box<dyn Error>>
+ *   (src/raytracing/camera.rs:223-227, called from src/raytracing/mod.rs:123)
+ * whose per-ray trait calls (Hittable::hit, hittable.rs:12-14; Material::scatter,
+ * materials.rs:7-9) are far too fine-grained to cross a device boundary. So the
+ * boundary is at whole-image granularity: the host flattens the scene (spheres +
+ * material table) and the derived Camera, and one call renders all pixels.
+ * The Rust-side binding a maintainer would add (bindgen + cc) is shown in
+ * INTEGRATION.md.
+ *
+ * All structs are POD and bindgen-clean. All calls are synchronous unless noted,
+ * return RTW_OK (0) or a negative RTW_E_* code, never abort, and leave a
+ * thread-local message in rtw_last_error(). The caller owns every host buffer for
+ * the duration of a call; nothing is retained after return.
+ */
+#ifndef RTW_CAPI_H
+#define RTW_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTW_ABI_VERSION 1
+
+/* ---- error codes ---- */
+#define RTW_OK 0
+#define RTW_E_ARG (-1)          /* null pointer / bad size / bad shard                 */
+#define RTW_E_EMPTY_IMAGE (-2)  /* height or width 0: assert!, camera.rs:267           */
+#define RTW_E_FUZZ (-3)         /* Metal fuzz > 1: assert!, materials.rs:47            */
+#define RTW_E_MAT_INDEX (-4)    /* sphere refers to a material that does not exist     */
+#define RTW_E_HIP (-5)          /* HIP runtime error (message in rtw_last_error)       */
+#define RTW_E_UNSUPPORTED (-6)  /* limits of this build (max_depth, table sizes)       */
+#define RTW_E_NO_DEVICE (-7)    /* no usable gfx950 device                             */
+#define RTW_E_CAPACITY (-8)     /* caller buffer too small (count written anyway)      */
+
+/* ---- plain data ---- */
+typedef struct rtw_vec3 { double x, y, z; } rtw_vec3;           /* Vec3/Point3/Color, vec3.rs:9-14 */
+typedef struct rtw_u128 { uint64_t lo, hi; } rtw_u128;          /* XorShift state, random.rs:3-6   */
+
+/* Camera after Camera::new (camera.rs:138-221): the derived values the path reads. */
+typedef struct rtw_camera {
+    uint32_t img_height, img_width, max_depth, _pad0;
+    double focal_length, fov;                 /* stored, unused by the path (as in the reference) */
+    rtw_vec3 look_from, look_to, vup;
+    rtw_vec3 u, v, w;                         /* BasisVecs, camera.rs:96-100                  */
+    double viewport_height, viewport_width;
+    rtw_vec3 pixel00, pixel_delta_u, pixel_delta_v;
+    double defocus_angle, focus_dist;
+    rtw_vec3 defocus_disk_u, defocus_disk_v;
+} rtw_camera;
+
+/* Material table row: Lambertian{albedo} (materials.rs:11-14), Metal{albedo,fuzz}
+ * (39-43), Dielectric{ir} (65-68). Unused fields are ignored. */
+enum { RTW_LAMBERTIAN = 0, RTW_METAL = 1, RTW_DIELECTRIC = 2 };
+typedef struct rtw_material {
+    uint32_t kind, _pad;
+    double albedo[3];
+    double fuzz;
+    double ir;
+} rtw_material;
+
+/* Sphere{center, radius, mat} (sphere.rs:11-16); mat indexes the material table. */
+typedef struct rtw_sphere {
+    double center[3];
+    double radius;
+    uint32_t mat, _pad;
+} rtw_sphere;
+
+/* Rows row_begin + k*row_step for k < n_rows (row-cyclic multi-GPU shards).
+ * NULL shard = the whole image. Output row k of a shard is image row
+ * row_begin + k*row_step; per-pixel RNG streams depend only on the global pixel
+ * index, so any shard reproduces the unsharded pixels bit-for-bit. */
+typedef struct rtw_shard { uint32_t row_begin, row_step, n_rows, _pad; } rtw_shard;
+
+typedef struct rtw_stats {
+    uint64_t pixels;          /* pixels rendered                                       */
+    uint64_t samples;         /* pixels x lattice offsets (samples_sqrt^2, or 1 if 0)  */
+    uint64_t segments;        /* traced segments = Scene::hit calls                    */
+    uint64_t sphere_tests;    /* segments x n_spheres (brute force, as the reference)  */
+    uint64_t wave_iterations; /* sum over waves of the wave's loop trip count          */
+    double kernel_ms;         /* render kernel time, HIP events on the launch stream   */
+    uint32_t grid_blocks, block_threads;
+} rtw_stats;
+
+/* ---- library ---- */
+const char *rtw_version(void);
+const char *rtw_last_error(void);
+int rtw_device_count(int *count);
+
+/* ---- host mirror of the reference types (bit-exact f64, no FMA) ---- */
+/* Camera::new(img_height, img_width, max_depth, focal_length, fov, look_from,
+ * look_to, vup, defocus_angle, focus_dist, None) -- camera.rs:138-150.
+ * Note the reference's argument order: height before width. */
+int rtw_camera_new(uint32_t img_height, uint32_t img_width, uint32_t max_depth,
+                   double focal_length, double fov, const rtw_vec3 *look_from,
+                   const rtw_vec3 *look_to, const rtw_vec3 *vup, double defocus_angle,
+                   double focus_dist, rtw_camera *out);
+
+/* Camera::offset_lattice(dx, dy, num_layers) -- camera.rs:422-450 (the render
+ * calls it as (pixel_delta_v, pixel_delta_u, s), camera.rs:243-244). */
+int rtw_offset_lattice(const rtw_vec3 *dx, const rtw_vec3 *dy, uint32_t samples_sqrt,
+                       rtw_vec3 *out, uint32_t cap, uint32_t *count);
+
+/* Interval::contains_inc / contains_ex -- interval.rs:55-62 */
+int rtw_interval_contains_inc(double min, double max, double x);
+int rtw_interval_contains_ex(double min, double max, double x);
+
+/* XorShift::next_int / next_01 streams from `seed` (random.rs:33-52). */
+int rtw_xorshift_next_int(rtw_u128 seed, uint32_t n, rtw_u128 *out);
+int rtw_xorshift_next_01(rtw_u128 seed, uint32_t n, double *out);
+/* Children handed to pixels first_pixel .. first_pixel+count-1 by the row-major
+ * copy_reset chain of threaded_render (camera.rs:255, 269-272; random.rs:61-69),
+ * computed by GF(2) jump-ahead (no serial walk). */
+int rtw_seed_children(rtw_u128 seed, uint64_t first_pixel, uint64_t count, rtw_u128 *out);
+
+/* Built-in scenes (raytracing/mod.rs). name: "complex" (54-126, the book's final
+ * scene; `seed` replaces the wall-clock XorShift::default at mod.rs:67),
+ * "simple" (129-173), "threads" (176-202), "super_simple" (205-238), and
+ * "three_lambertian" (BASELINE config 1: simple() with the dielectric dropped and
+ * the metal sphere made Lambertian). img_height/img_width/max_depth override the
+ * builder's hard-coded values when non-zero. Writes up to `cap` spheres and
+ * materials; *n_spheres / *n_mats receive the full counts. */
+int rtw_scene_builtin(const char *name, rtw_u128 seed, uint32_t img_height, uint32_t img_width,
+                      uint32_t max_depth, rtw_camera *cam, rtw_sphere *spheres,
+                      rtw_material *mats, uint32_t cap, uint32_t *n_spheres, uint32_t *n_mats);
+
+/* Color::wire_full_file (color.rs:196-247) on an H*W*3 f64 framebuffer (row 0 =
+ * top). rtw_format_ppm returns the byte count (writes only if buf && cap
+ * suffice); rtw_write_ppm writes the file. */
+int64_t rtw_format_ppm(const double *rgb, uint32_t width, uint32_t height, char *buf,
+                       uint64_t cap);
+int rtw_write_ppm(const char *path, const double *rgb, uint32_t width, uint32_t height);
+
+/* ---- the hot path ---- */
+/* Camera::threaded_render equivalent: renders `shard` (NULL = all rows) of the
+ * scene into out_rgb (host, n_rows*W*3 f64, row-major), on device 0 (or
+ * $RTW_DEVICE). Per-pixel RNG: child p of `seed` (random.rs:61-69). Validation
+ * mirrors the reference's asserts. stats may be NULL. */
+int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                        const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                        rtw_u128 seed, const rtw_shard *shard, double *out_rgb,
+                        rtw_stats *stats);
+
+/* Device-resident sessions: scene uploaded once, renders enqueued on a caller
+ * stream into a caller device buffer (inputs already in HBM when timing). */
+typedef struct rtw_session rtw_session;
+int rtw_session_create(int device, rtw_session **out);
+int rtw_session_destroy(rtw_session *s);
+int rtw_session_set_scene(rtw_session *s, const rtw_sphere *spheres, uint32_t n_spheres,
+                          const rtw_material *mats, uint32_t n_mats);
+/* Asynchronous: enqueues the render of `shard` on `hip_stream` (a hipStream_t;
+ * NULL = the session's own stream) writing out_rgb_device (device pointer,
+ * n_rows*W*3 f64). */
+int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
+                       rtw_u128 seed, const rtw_shard *shard, double *out_rgb_device,
+                       void *hip_stream);
+/* Waits for the session's last render and reports its statistics. */
+int rtw_session_stats(rtw_session *s, rtw_stats *out);
+
+/* ---- device probes (tests) ---- */
+/* Device jump-ahead seeds (the kernel's own code path) for a pixel range. */
+int rtw_probe_device_seeds(int device, rtw_u128 seed, uint64_t first_pixel, uint64_t count,
+                           rtw_u128 *out);
+/* Device f64 sqrt(a) and a/b, to check correct rounding against the host. */
+int rtw_probe_f64_ops(int device, const double *a, const double *b, uint64_t n,
+                      double *out_sqrt, double *out_div);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTW_CAPI_H */

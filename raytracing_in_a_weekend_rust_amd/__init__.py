@@ -1,0 +1,10 @@
+"""MI355X-native (gfx950 HIP) implementation of the per-pixel sampling hot path of
+NicoElbers/Raytracing_in_a_weekend_rust (Camera::threaded_render -> ray_color ->
+Scene::hit / Sphere::hit -> Material::scatter), behind the C ABI in
+include/rtw_capi.h. See DESIGN.md."""
+from ._capi import LIB_PATH, RtwError  # noqa: F401  (raises ImportError if librtw.so is missing)
+from .api import (DEFAULT_SEED, Camera, Dielectric, Lambertian, Metal, Scene,  # noqa: F401
+                  SceneBuilder, Session, Sphere, builtin_scene, device_count, format_ppm,
+                  render_flat, seed_children, write_ppm, xorshift_next_01, xorshift_next_int)
+
+__version__ = "0.1.0"

@@ -1,0 +1,735 @@
+// rtw_render.hip -- CDNA4 (gfx950) path-tracing megakernel for the reference's
+// per-pixel sampling hot path, plus the device half of the C ABI.
+//
+// Replaces Camera::threaded_render's per-pixel job loop (camera.rs:269-292),
+// ray_colors_lattice (354-374), the ray_color recursion (376-398), get_ray /
+// offset_lattice / defocus_disk_sample (400-456), Scene::hit (hittable.rs:131-143),
+// Sphere::hit (sphere.rs:39-71) and the three Material::scatter impls
+// (materials.rs:22-111).
+//
+// Parity mode (the only mode in this build): f64 everywhere, compiled with
+// -ffp-contract=off so no a*b+c is fused; every expression is evaluated in the
+// reference's order, division and sqrt are IEEE (checked on the box by
+// rtw_probe_f64_ops). The RNG is the reference's u128 xorshift(23,17,26), bit-exact.
+//
+// Layout: one work-item per pixel, a 256-thread workgroup = a 16x16 pixel tile
+// (each wave64 = 16x4 pixels, neighbours with similar path lengths). The sphere
+// list {cx,cy,cz,r*r} (32 B each) is staged in LDS once per workgroup and read
+// with wave-uniform broadcasts; radius, material index and the material table stay
+// in HBM (read once per hit). Each lane runs a flattened sample x bounce loop:
+// one brute-force intersection pass per iteration, then scatter or finish the
+// sample and generate the next; the wave retires when all its lanes are done.
+// The ray_color product att0*(att1*(...*leaf)) is formed right-to-left from a
+// per-lane stack of material indices, so it associates exactly as the recursion.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rtw_capi.h"
+#include "host/rtw_host.h"
+#include "host/rtw_internal.h"
+
+namespace {
+
+constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
+constexpr int kTile = 16;
+constexpr uint32_t kLdsSphereCap = 2048;  // 64 KiB of {cx,cy,cz,r*r}
+
+struct U128 {
+    uint64_t lo, hi;
+};
+
+struct KParams {
+    double p00[3], du[3], dv[3], from[3], ddu[3], ddv[3];
+    double lat_dx[3], lat_dy[3], lat_pos0[3];  // lattice step (delta_v/s, delta_u/s) and pos0
+    double defocus_angle;
+    uint32_t W, s, n_off, max_depth;
+    uint32_t row_begin, row_step, n_rows, n_sph;
+    uint32_t jump_bits, _pad;
+    uint64_t seed_lo, seed_hi;
+    const double4 *sph;         // {cx, cy, cz, r*r}
+    const double *radius;       // r
+    const uint32_t *sph_mat;    // material row per sphere
+    const rtw_material *mats;   // material table
+    const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
+    double *out;                // n_rows * W * 3
+    unsigned long long *counters;  // [0] segments, [1] wave iterations
+};
+
+// ------------------------------------------------------------------ XorShift --
+// random.rs:33-38 on (lo, hi) halves
+__device__ __forceinline__ void xs_step(U128 &s) {
+    uint64_t hi = s.hi ^ ((s.hi << 23) | (s.lo >> 41));
+    uint64_t lo = s.lo ^ (s.lo << 23);
+    lo ^= (lo >> 17) | (hi << 47);
+    hi ^= hi >> 17;
+    hi ^= (hi << 26) | (lo >> 38);
+    lo ^= lo << 26;
+    s.lo = lo;
+    s.hi = hi;
+}
+// random.rs:40-52: u128 % (2^32-1) by limb folding (2^32 == 1 mod 2^32-1),
+// then an IEEE f64 divide (not a reciprocal multiply).
+__device__ __forceinline__ double xs_next_01(U128 &s) {
+    xs_step(s);
+    uint64_t t = (s.lo & 0xffffffffull) + (s.lo >> 32) + (s.hi & 0xffffffffull) + (s.hi >> 32);
+    t = (t & 0xffffffffull) + (t >> 32);
+    t = (t & 0xffffffffull) + (t >> 32);
+    const uint32_t m = t == 0xffffffffull ? 0u : static_cast<uint32_t>(t);
+    return static_cast<double>(m) / 4294967295.0;
+}
+// random.rs:61-69: the child handed out by copy_reset at parent state p
+__device__ __forceinline__ U128 child_of(U128 p) {
+    U128 n = p;
+    xs_step(n);
+    uint64_t lo = p.lo ^ n.lo, hi = p.hi ^ n.hi;
+    lo ^= (lo >> 13) | (hi << 51);
+    hi ^= hi >> 13;
+    hi ^= (hi << 5) | (lo >> 59);
+    lo ^= lo << 5;
+    lo ^= (lo >> 11) | (hi << 53);
+    hi ^= hi >> 11;
+    return U128{lo, hi};
+}
+// Parent state before pixel p = T^p(seed) (the serial chain of camera.rs:269-272),
+// by GF(2) jump-ahead: wave-uniform column loads, per-lane masked XOR.
+__device__ __forceinline__ U128 jump_state(U128 s, uint64_t p, const uint4 *__restrict__ tab,
+                                           uint32_t bits) {
+    for (uint32_t k = 0; k < bits; ++k) {
+        const uint4 *cols = tab + k * 128u;
+        uint64_t rlo = 0, rhi = 0;
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t m = 0ull - ((s.lo >> j) & 1ull);
+            const uint4 c = cols[j];
+            rlo ^= m & ((static_cast<uint64_t>(c.y) << 32) | c.x);
+            rhi ^= m & ((static_cast<uint64_t>(c.w) << 32) | c.z);
+        }
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) {
+            const uint64_t m = 0ull - ((s.hi >> j) & 1ull);
+            const uint4 c = cols[64 + j];
+            rlo ^= m & ((static_cast<uint64_t>(c.y) << 32) | c.x);
+            rhi ^= m & ((static_cast<uint64_t>(c.w) << 32) | c.z);
+        }
+        if ((p >> k) & 1ull) {
+            s.lo = rlo;
+            s.hi = rhi;
+        }
+    }
+    return s;
+}
+
+// vec3.rs:207-232: rejection in [-1,1]^3 with len^2 <= 1, then / sqrt(len^2)
+__device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &uy, double &uz) {
+    double x, y, z, l2;
+    do {
+        x = -1. + xs_next_01(rng) * 2.;
+        y = -1. + xs_next_01(rng) * 2.;
+        z = -1. + xs_next_01(rng) * 2.;
+        l2 = x * x + y * y + z * z;
+    } while (!(l2 <= 1.));
+    const double l = __builtin_sqrt(l2);
+    ux = x / l;
+    uy = y / l;
+    uz = z / l;
+}
+
+// ---------------------------------------------------------------- megakernel --
+template <int CAP, bool kLds>
+__global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
+    extern __shared__ double4 lds_sph[];
+    const double4 *__restrict__ sph = kLds ? lds_sph : P.sph;
+    if (kLds) {
+        for (uint32_t i = threadIdx.x; i < P.n_sph; i += kBlock) lds_sph[i] = P.sph[i];
+        __syncthreads();
+    }
+
+    const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
+    const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
+    uint32_t seg = 0;
+
+    if (x < P.W && lr < P.n_rows) {
+        const uint32_t y = P.row_begin + lr * P.row_step;
+        U128 rng = child_of(jump_state(U128{P.seed_lo, P.seed_hi},
+                                       static_cast<uint64_t>(y) * P.W + x, P.jump, P.jump_bits));
+
+        // get_ray, camera.rs:403: (pixel00 + i*du) + j*dv
+        const double fx = static_cast<double>(x), fy = static_cast<double>(y);
+        const double plx = (P.p00[0] + P.du[0] * fx) + P.dv[0] * fy;
+        const double ply = (P.p00[1] + P.du[1] * fx) + P.dv[1] * fy;
+        const double plz = (P.p00[2] + P.du[2] * fx) + P.dv[2] * fy;
+
+        double ox, oy, oz, dx, dy, dz;
+        // camera.rs:400-420 + offset_lattice (422-450) + defocus_disk_sample (452-456)
+        auto gen_ray = [&](uint32_t k) {
+            double offx, offy, offz;
+            if (P.s == 0) {
+                offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
+            } else {
+                const uint32_t ly = k / P.s, lx = k - ly * P.s;
+                const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
+                offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
+                offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
+                offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
+            }
+            const double sx = plx + offx, sy = ply + offy, sz = plz + offz;
+            if (P.defocus_angle <= 0.) {
+                ox = P.from[0], oy = P.from[1], oz = P.from[2];
+            } else {
+                double px, py;
+                do {  // vec3.rs:270-277: strict len^2 < 1
+                    px = -1. + 2. * xs_next_01(rng);
+                    py = -1. + 2. * xs_next_01(rng);
+                } while (!((px * px + py * py + 0. * 0.) < 1.));
+                ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
+                oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
+                oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
+            }
+            dx = sx - ox, dy = sy - oy, dz = sz - oz;
+        };
+
+        double accr = 0., accg = 0., accb = 0.;
+        const uint32_t n_off = P.n_off;
+        if (P.max_depth == 0) {  // every sample is black, RNG still consumed by get_ray
+            for (uint32_t k = 0; k < n_off; ++k) gen_ray(k);
+        } else {
+            uint16_t stk[CAP];
+            uint32_t nst = 0, depth = 0, k = 0;
+            gen_ray(0);
+            for (;;) {
+                // ---- Scene::hit: all spheres, first minimum wins ----
+                ++seg;
+                const double a = dx * dx + dy * dy + dz * dz;
+                int best = -1;
+                double bt = 0.;
+                for (uint32_t i = 0; i < P.n_sph; ++i) {
+                    const double4 S = sph[i];
+                    const double ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
+                    const double hb = ocx * dx + ocy * dy + ocz * dz;
+                    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - S.w;
+                    const double disc = hb * hb - a * c;
+                    if (!(disc < 0.)) {
+                        const double sq = __builtin_sqrt(disc);
+                        double t = (-sq - hb) / a;
+                        if (!(t >= 0.01)) t = (sq - hb) / a;
+                        if (t >= 0.01 && (best < 0 || t < bt)) {
+                            bt = t;
+                            best = static_cast<int>(i);
+                        }
+                    }
+                }
+
+                bool finish;
+                double lr_ = 0., lg = 0., lb = 0.;
+                if (best >= 0) {
+                    // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
+                    const double4 S = sph[best];
+                    const double r = P.radius[best];
+                    const double px = dx * bt + ox, py = dy * bt + oy, pz = dz * bt + oz;
+                    double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
+                    const bool front = (dx * nx + dy * ny + dz * nz) < 0.;
+                    if (!front) nx = -nx, ny = -ny, nz = -nz;
+                    const uint32_t mi = P.sph_mat[best];
+                    const rtw_material M = P.mats[mi];
+                    double ndx, ndy, ndz;
+                    if (M.kind == RTW_LAMBERTIAN) {  // materials.rs:22-37
+                        double ux, uy, uz;
+                        random_unit_vec(rng, ux, uy, uz);
+                        ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
+                        if (ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = nx, ndy = ny, ndz = nz;
+                        stk[nst++] = static_cast<uint16_t>(mi);
+                    } else if (M.kind == RTW_METAL) {  // materials.rs:52-63
+                        const double l = __builtin_sqrt(a);
+                        const double vx = dx / l, vy = dy / l, vz = dz / l;
+                        const double dt = vx * nx + vy * ny + vz * nz;
+                        const double rx = vx - (nx * dt) * 2., ry = vy - (ny * dt) * 2.,
+                                     rz = vz - (nz * dt) * 2.;
+                        double ux, uy, uz;
+                        random_unit_vec(rng, ux, uy, uz);
+                        ndx = rx + ux * M.fuzz, ndy = ry + uy * M.fuzz, ndz = rz + uz * M.fuzz;
+                        stk[nst++] = static_cast<uint16_t>(mi);
+                    } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
+                        const double ratio = front ? 1. / M.ir : M.ir;
+                        const double l = __builtin_sqrt(a);
+                        const double vx = dx / l, vy = dy / l, vz = dz / l;
+                        const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+                        const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+                        bool refl = ratio * sin_t > 1.;
+                        if (!refl) {
+                            double r0 = (1. - M.ir) / (1. + M.ir);
+                            r0 = r0 * r0;
+                            const double q = 1. - cos_t;
+                            const double schlick = r0 + (1. - r0) * (q * ((q * q) * (q * q)));
+                            refl = schlick > xs_next_01(rng);
+                        }
+                        if (refl) {  // vec3.rs:252-257
+                            const double dt = vx * nx + vy * ny + vz * nz;
+                            ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2.,
+                            ndz = vz - (nz * dt) * 2.;
+                        } else {  // vec3.rs:259-268
+                            const double ct = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+                            const double qx = (vx + nx * ct) * ratio, qy = (vy + ny * ct) * ratio,
+                                         qz = (vz + nz * ct) * ratio;
+                            const double w =
+                                -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
+                            ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
+                        }
+                    }
+                    ox = px, oy = py, oz = pz;
+                    dx = ndx, dy = ndy, dz = ndz;
+                    ++depth;
+                    finish = depth >= P.max_depth;  // ray_color(depth >= max) -> black
+                } else {
+                    // sky, camera.rs:395-397
+                    const double uy = dy / __builtin_sqrt(a);
+                    const double t = 0.5 * (uy + 1.0);
+                    const double om = 1.0 - t;
+                    lr_ = om + 0.5 * t;
+                    lg = om + 0.7 * t;
+                    lb = om + t;
+                    finish = true;
+                }
+
+                if (finish) {
+                    // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion
+                    while (nst > 0) {
+                        const rtw_material &A = P.mats[stk[--nst]];
+                        lr_ = A.albedo[0] * lr_;
+                        lg = A.albedo[1] * lg;
+                        lb = A.albedo[2] * lb;
+                    }
+                    accr = accr + lr_, accg = accg + lg, accb = accb + lb;
+                    if (++k >= n_off) break;
+                    depth = 0;
+                    gen_ray(k);
+                }
+            }
+        }
+        const double nf = static_cast<double>(n_off);
+        double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
+        o[0] = accr / nf;
+        o[1] = accg / nf;
+        o[2] = accb / nf;
+    }
+
+    // segments (atomic, wave-reduced by the compiler) and the wave's trip count
+    if (P.counters) {
+        if (seg) atomicAdd(&P.counters[0], static_cast<unsigned long long>(seg));
+        uint32_t m = seg;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&P.counters[1], static_cast<unsigned long long>(m));
+    }
+}
+
+// ------------------------------------------------------------------- probes --
+__global__ void probe_seeds(U128 seed, uint64_t first, uint64_t count, const uint4 *tab,
+                            uint32_t bits, U128 *out) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < count) out[i] = child_of(jump_state(seed, first + i, tab, bits));
+}
+__global__ void probe_f64(const double *a, const double *b, uint64_t n, double *osq, double *odiv) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        osq[i] = __builtin_sqrt(a[i]);
+        odiv[i] = a[i] / b[i];
+    }
+}
+
+// ------------------------------------------------------------------- host ---
+#define HIPCHECK(expr)                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            throw rtw::Error(RTW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+uint32_t bit_length(uint64_t v) {
+    uint32_t b = 0;
+    while (v) ++b, v >>= 1;
+    return b;
+}
+
+}  // namespace
+
+struct rtw_session {
+    int device = 0;
+    hipStream_t own = nullptr;
+    double4 *d_sph = nullptr;
+    double *d_rad = nullptr;
+    uint32_t *d_smat = nullptr;
+    rtw_material *d_mats = nullptr;
+    uint4 *d_jump = nullptr;
+    unsigned long long *d_counters = nullptr;
+    uint32_t n_sph = 0, n_mats = 0;
+    bool scene_set = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool pending = false;
+    rtw_stats last{};
+};
+
+namespace {
+
+void dev_free(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+void upload_jump(rtw_session *s) {
+    const auto &t = rtw::jump_table();
+    std::vector<uint4> cols(t.size());
+    for (size_t i = 0; i < t.size(); ++i) {
+        const uint64_t lo = static_cast<uint64_t>(t[i]), hi = static_cast<uint64_t>(t[i] >> 64);
+        cols[i] = make_uint4(static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32),
+                             static_cast<uint32_t>(hi), static_cast<uint32_t>(hi >> 32));
+    }
+    HIPCHECK(hipMalloc(&s->d_jump, cols.size() * sizeof(uint4)));
+    HIPCHECK(hipMemcpy(s->d_jump, cols.data(), cols.size() * sizeof(uint4), hipMemcpyHostToDevice));
+}
+
+void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
+    if ((n && !sp) || (nm && !m)) throw rtw::Error(RTW_E_ARG, "null scene buffer");
+    if (nm > 65536) throw rtw::Error(RTW_E_UNSUPPORTED, "more than 65536 materials");
+    for (uint32_t i = 0; i < nm; ++i) {
+        if (m[i].kind > RTW_DIELECTRIC) throw rtw::Error(RTW_E_ARG, "unknown material kind");
+        if (m[i].kind == RTW_METAL && !(m[i].fuzz <= 1.))
+            throw rtw::Error(RTW_E_FUZZ, "Fuzz cannot be more than 1");  // materials.rs:47
+    }
+    for (uint32_t i = 0; i < n; ++i)
+        if (sp[i].mat >= nm) throw rtw::Error(RTW_E_MAT_INDEX, "sphere material index out of range");
+}
+
+void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
+    validate_scene(sp, n, m, nm);
+    HIPCHECK(hipSetDevice(s->device));
+    dev_free(s->d_sph), dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    s->d_sph = nullptr, s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
+    std::vector<double4> a(n ? n : 1);
+    std::vector<double> r(n ? n : 1);
+    std::vector<uint32_t> mi(n ? n : 1);
+    for (uint32_t i = 0; i < n; ++i) {
+        const double rad = sp[i].radius;
+        a[i] = make_double4(sp[i].center[0], sp[i].center[1], sp[i].center[2], rad * rad);
+        r[i] = rad;
+        mi[i] = sp[i].mat;
+    }
+    HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
+    HIPCHECK(hipMalloc(&s->d_rad, r.size() * sizeof(double)));
+    HIPCHECK(hipMalloc(&s->d_smat, mi.size() * sizeof(uint32_t)));
+    HIPCHECK(hipMalloc(&s->d_mats, (nm ? nm : 1) * sizeof(rtw_material)));
+    HIPCHECK(hipMemcpy(s->d_sph, a.data(), a.size() * sizeof(double4), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_rad, r.data(), r.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_smat, mi.data(), mi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (nm) HIPCHECK(hipMemcpy(s->d_mats, m, nm * sizeof(rtw_material), hipMemcpyHostToDevice));
+    s->n_sph = n;
+    s->n_mats = nm;
+    s->scene_set = true;
+}
+
+rtw_shard resolve_shard(const rtw_camera *cam, const rtw_shard *shard) {
+    rtw_shard sh{0, 1, cam->img_height, 0};
+    if (shard) {
+        sh = *shard;
+        if (sh.row_step == 0) throw rtw::Error(RTW_E_ARG, "shard row_step must be > 0");
+        if (sh.n_rows && static_cast<uint64_t>(sh.row_begin) +
+                                 static_cast<uint64_t>(sh.n_rows - 1) * sh.row_step >=
+                             cam->img_height)
+            throw rtw::Error(RTW_E_ARG, "shard rows outside the image");
+    }
+    return sh;
+}
+
+void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+            const rtw_shard *shard_in, double *out, hipStream_t stream) {
+    if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
+    if (!s->scene_set) throw rtw::Error(RTW_E_ARG, "session has no scene");
+    if (cam->img_height == 0 || cam->img_width == 0)
+        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");  // camera.rs:267
+    if (cam->max_depth > 1024) throw rtw::Error(RTW_E_UNSUPPORTED, "max_depth > 1024");
+    if (samples_sqrt > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "samples_sqrt > 65535");
+    const uint64_t npix = static_cast<uint64_t>(cam->img_height) * cam->img_width;
+    const uint32_t bits = bit_length(npix - 1);
+    if (bits > static_cast<uint32_t>(rtw::kJumpBits)) throw rtw::Error(RTW_E_UNSUPPORTED, "image > 2^40 pixels");
+    const rtw_shard sh = resolve_shard(cam, shard_in);
+
+    KParams P{};
+    auto cp = [](double *d, const rtw_vec3 &v) { d[0] = v.x, d[1] = v.y, d[2] = v.z; };
+    cp(P.p00, cam->pixel00);
+    cp(P.du, cam->pixel_delta_u);
+    cp(P.dv, cam->pixel_delta_v);
+    cp(P.from, cam->look_from);
+    cp(P.ddu, cam->defocus_disk_u);
+    cp(P.ddv, cam->defocus_disk_v);
+    // offset_lattice(&pixel_delta_v, &pixel_delta_u, s) (camera.rs:243-244): dx := delta_v
+    const rtw::Vec3 dxv = rtw::Vec3::of(cam->pixel_delta_v), dyv = rtw::Vec3::of(cam->pixel_delta_u);
+    if (samples_sqrt == 0) {
+        cp(P.lat_pos0, (dxv / 2. + dyv / 2.).c());
+    } else {
+        const double n = static_cast<double>(samples_sqrt);
+        const rtw::Vec3 dx = dxv / n, dy = dyv / n;
+        cp(P.lat_dx, dx.c());
+        cp(P.lat_dy, dy.c());
+        cp(P.lat_pos0, (dx / 2. + dy / 2.).c());
+    }
+    P.defocus_angle = cam->defocus_angle;
+    P.W = cam->img_width;
+    P.s = samples_sqrt;
+    P.n_off = samples_sqrt ? samples_sqrt * samples_sqrt : 1;
+    P.max_depth = cam->max_depth;
+    P.row_begin = sh.row_begin;
+    P.row_step = sh.row_step;
+    P.n_rows = sh.n_rows;
+    P.n_sph = s->n_sph;
+    P.jump_bits = bits;
+    P.seed_lo = seed.lo;
+    P.seed_hi = seed.hi;
+    P.sph = s->d_sph;
+    P.radius = s->d_rad;
+    P.sph_mat = s->d_smat;
+    P.mats = s->d_mats;
+    P.jump = s->d_jump;
+    P.out = out;
+    P.counters = s->d_counters;
+
+    HIPCHECK(hipSetDevice(s->device));
+    hipStream_t st = stream ? stream : s->own;
+    const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
+    const bool use_lds = P.n_sph <= kLdsSphereCap;
+    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * sizeof(double4) : 0;
+    HIPCHECK(hipMemsetAsync(s->d_counters, 0, 2 * sizeof(unsigned long long), st));
+    HIPCHECK(hipEventRecord(s->ev0, st));
+    if (P.n_rows) {
+        if (P.max_depth <= 64) {
+            if (use_lds) hipLaunchKernelGGL((rtw_render_f64<64, true>), grid, dim3(kBlock), lds, st, P);
+            else hipLaunchKernelGGL((rtw_render_f64<64, false>), grid, dim3(kBlock), 0, st, P);
+        } else {
+            if (use_lds) hipLaunchKernelGGL((rtw_render_f64<1024, true>), grid, dim3(kBlock), lds, st, P);
+            else hipLaunchKernelGGL((rtw_render_f64<1024, false>), grid, dim3(kBlock), 0, st, P);
+        }
+        HIPCHECK(hipGetLastError());
+    }
+    HIPCHECK(hipEventRecord(s->ev1, st));
+    s->last_stream = st;
+    s->pending = true;
+    s->last = rtw_stats{};
+    s->last.pixels = static_cast<uint64_t>(P.n_rows) * P.W;
+    s->last.samples = s->last.pixels * P.n_off;
+    s->last.grid_blocks = grid.x * grid.y;
+    s->last.block_threads = kBlock;
+}
+
+void collect(rtw_session *s) {
+    if (!s->pending) return;
+    HIPCHECK(hipSetDevice(s->device));
+    HIPCHECK(hipEventSynchronize(s->ev1));
+    unsigned long long c[2] = {0, 0};
+    HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+    float ms = 0.f;
+    HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+    s->last.segments = c[0];
+    s->last.wave_iterations = c[1];
+    s->last.sphere_tests = c[0] * s->n_sph;
+    s->last.kernel_ms = ms;
+    s->pending = false;
+}
+
+int default_device() {
+    const char *e = std::getenv("RTW_DEVICE");
+    return e ? std::atoi(e) : 0;
+}
+
+void create_session(int device, rtw_session **out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw rtw::Error(RTW_E_NO_DEVICE, "no HIP device");
+    if (device < 0 || device >= n) throw rtw::Error(RTW_E_NO_DEVICE, "device index out of range");
+    auto *s = new rtw_session();
+    s->device = device;
+    try {
+        HIPCHECK(hipSetDevice(device));
+        HIPCHECK(hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreate(&s->ev0));
+        HIPCHECK(hipEventCreate(&s->ev1));
+        HIPCHECK(hipMalloc(&s->d_counters, 2 * sizeof(unsigned long long)));
+        upload_jump(s);
+    } catch (...) {
+        rtw_session_destroy(s);
+        throw;
+    }
+    *out = s;
+}
+
+}  // namespace
+
+#define RTW_GUARD_BEGIN try {
+#define RTW_GUARD_END                         \
+    }                                         \
+    catch (const rtw::Error &e) {             \
+        rtw::set_error(e.what());             \
+        return e.code;                        \
+    }                                         \
+    catch (const std::exception &e) {         \
+        rtw::set_error(e.what());             \
+        return RTW_E_ARG;                     \
+    }
+
+extern "C" {
+
+int rtw_device_count(int *count) {
+    if (!count) return rtw::set_error("null argument"), RTW_E_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RTW_OK;
+}
+
+int rtw_session_create(int device, rtw_session **out) {
+    if (!out) return rtw::set_error("null argument"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    create_session(device, out);
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_session_destroy(rtw_session *s) {
+    if (!s) return RTW_OK;
+    (void)hipSetDevice(s->device);
+    if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
+    dev_free(s->d_sph), dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    dev_free(s->d_jump), dev_free(s->d_counters);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->own) (void)hipStreamDestroy(s->own);
+    delete s;
+    return RTW_OK;
+}
+
+int rtw_session_set_scene(rtw_session *s, const rtw_sphere *spheres, uint32_t n_spheres,
+                          const rtw_material *mats, uint32_t n_mats) {
+    if (!s) return rtw::set_error("null session"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    set_scene(s, spheres, n_spheres, mats, n_mats);
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
+                       rtw_u128 seed, const rtw_shard *shard, double *out_rgb_device,
+                       void *hip_stream) {
+    if (!s) return rtw::set_error("null session"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    render(s, cam, samples_sqrt, seed, shard, out_rgb_device, static_cast<hipStream_t>(hip_stream));
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_session_stats(rtw_session *s, rtw_stats *out) {
+    if (!s || !out) return rtw::set_error("null argument"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    collect(s);
+    *out = s->last;
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                        const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                        rtw_u128 seed, const rtw_shard *shard, double *out_rgb, rtw_stats *stats) {
+    if (!cam || !out_rgb) return rtw::set_error("null argument"), RTW_E_ARG;
+    static std::mutex mu;
+    static rtw_session *cached = nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    double *d_out = nullptr;
+    RTW_GUARD_BEGIN
+    if (cam->img_height == 0 || cam->img_width == 0)
+        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
+    validate_scene(spheres, n_spheres, mats, n_mats);
+    const rtw_shard sh = resolve_shard(cam, shard);
+    const int dev = default_device();
+    if (cached && cached->device != dev) rtw_session_destroy(cached), cached = nullptr;
+    if (!cached) create_session(dev, &cached);
+    set_scene(cached, spheres, n_spheres, mats, n_mats);
+    const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(double);
+    HIPCHECK(hipMalloc(&d_out, bytes ? bytes : 8));
+    render(cached, cam, samples_sqrt, seed, &sh, d_out, nullptr);
+    collect(cached);
+    if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
+    HIPCHECK(hipFree(d_out));
+    d_out = nullptr;
+    if (stats) *stats = cached->last;
+    return RTW_OK;
+    }
+    catch (const rtw::Error &e) {
+        if (d_out) (void)hipFree(d_out);
+        rtw::set_error(e.what());
+        return e.code;
+    }
+    catch (const std::exception &e) {
+        if (d_out) (void)hipFree(d_out);
+        rtw::set_error(e.what());
+        return RTW_E_ARG;
+    }
+}
+
+int rtw_probe_device_seeds(int device, rtw_u128 seed, uint64_t first_pixel, uint64_t count,
+                           rtw_u128 *out) {
+    if (!out && count) return rtw::set_error("null argument"), RTW_E_ARG;
+    rtw_session *s = nullptr;
+    U128 *d = nullptr;
+    RTW_GUARD_BEGIN
+    if (!count) return RTW_OK;
+    const uint32_t bits = bit_length(first_pixel + count - 1);
+    if (bits > static_cast<uint32_t>(rtw::kJumpBits)) throw rtw::Error(RTW_E_UNSUPPORTED, "pixel index beyond 2^40");
+    create_session(device, &s);
+    HIPCHECK(hipMalloc(&d, count * sizeof(U128)));
+    const unsigned blocks = static_cast<unsigned>((count + 255) / 256);
+    hipLaunchKernelGGL(probe_seeds, dim3(blocks), dim3(256), 0, s->own, U128{seed.lo, seed.hi},
+                       first_pixel, count, s->d_jump, bits, d);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(s->own));
+    HIPCHECK(hipMemcpy(out, d, count * sizeof(U128), hipMemcpyDeviceToHost));
+    HIPCHECK(hipFree(d));
+    rtw_session_destroy(s);
+    return RTW_OK;
+    }
+    catch (const rtw::Error &e) {
+        if (d) (void)hipFree(d);
+        rtw_session_destroy(s);
+        rtw::set_error(e.what());
+        return e.code;
+    }
+}
+
+int rtw_probe_f64_ops(int device, const double *a, const double *b, uint64_t n, double *out_sqrt,
+                      double *out_div) {
+    if ((!a || !b || !out_sqrt || !out_div) && n) return rtw::set_error("null argument"), RTW_E_ARG;
+    double *d = nullptr;
+    RTW_GUARD_BEGIN
+    if (!n) return RTW_OK;
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || device < 0 || device >= cnt)
+        throw rtw::Error(RTW_E_NO_DEVICE, "no such HIP device");
+    HIPCHECK(hipSetDevice(device));
+    HIPCHECK(hipMalloc(&d, 4 * n * sizeof(double)));
+    HIPCHECK(hipMemcpy(d, a, n * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d + n, b, n * sizeof(double), hipMemcpyHostToDevice));
+    const unsigned blocks = static_cast<unsigned>((n + 255) / 256);
+    hipLaunchKernelGGL(probe_f64, dim3(blocks), dim3(256), 0, nullptr, d, d + n, n, d + 2 * n, d + 3 * n);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipDeviceSynchronize());
+    HIPCHECK(hipMemcpy(out_sqrt, d + 2 * n, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(out_div, d + 3 * n, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipFree(d));
+    return RTW_OK;
+    }
+    catch (const rtw::Error &e) {
+        if (d) (void)hipFree(d);
+        rtw::set_error(e.what());
+        return e.code;
+    }
+}
+
+}  // extern "C"
