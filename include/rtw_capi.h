@@ -157,8 +157,8 @@ int rtw_session_destroy(rtw_session *s);
 int rtw_session_set_scene(rtw_session *s, const rtw_sphere *spheres, uint32_t n_spheres,
                           const rtw_material *mats, uint32_t n_mats);
 /* Asynchronous: enqueues the render of `shard` on `hip_stream` (a hipStream_t;
- * NULL = the session's own stream) writing out_rgb_device (device pointer,
- * n_rows*W*3 f64). */
+ * NULL = HIP's null stream, as everywhere in HIP) writing out_rgb_device (device
+ * pointer, n_rows*W*3 f64). */
 int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
                        rtw_u128 seed, const rtw_shard *shard, double *out_rgb_device,
                        void *hip_stream);

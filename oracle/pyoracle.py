@@ -343,6 +343,14 @@ def render(cam, objs, samples_sqrt, seed, rows=None):
     return out, stats[0]
 
 
+def cpow(x, y):
+    """libm pow (Rust f64::powf): NaN for a negative base with a fractional exponent."""
+    try:
+        return math.pow(x, y)
+    except ValueError:
+        return math.nan
+
+
 def format_ppm(img, w, h) -> str:  # color.rs:196-247
     def sat(v):
         if not (v > 0.0):
@@ -356,7 +364,39 @@ def format_ppm(img, w, h) -> str:  # color.rs:196-247
         vals = []
         for x in range(w):
             for c in img[(x, y)]:
-                vals.append(str(sat(math.pow(c, 1.0 / 2.2) * 255.0)))
+                vals.append(str(sat(cpow(c, 1.0 / 2.2) * 255.0)))
         if vals:
             lines.append(" ".join(vals) + "\n")
     return "".join(lines)
+
+
+# ----------------------------------------------------------- scene presets --
+def scene_builtin(name: str, seed: int, h=0, w=0, max_depth=0):
+    """raytracing/mod.rs builders (+ BASELINE config 1 'three_lambertian').
+    Returns (Camera, objs). Zero h/w/max_depth take the builder's own values."""
+    def pick(v, d):
+        return v if v else d
+
+    L = LAMBERTIAN
+    if name == "complex":  # mod.rs:54-126, Config defaults 1080x1920 (main.rs:20-29)
+        cam = Camera(pick(h, 1080), pick(w, 1920), pick(max_depth, 10), 1.0, 20.0,
+                     (13.0, 2.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 0.6, 10.0)
+        return cam, scene_complex(seed)
+    if name in ("simple", "three_lambertian"):  # mod.rs:129-173
+        three = name == "three_lambertian"
+        cam = Camera(pick(h, 225 if three else 1080), pick(w, 400 if three else 1920),
+                     pick(max_depth, 8 if three else 25), 1.0, 20.0, (-2.0, 2.0, 1.0),
+                     (0.0, 0.0, -1.0), (0.0, 1.0, 0.0), 10.0, 3.4)
+        objs = [((0.0, -100.5, -1.0), 100.0, (L, (0.8, 0.8, 0.0), 0.0, 0.0)),
+                ((0.0, 0.0, -1.0), 0.5, (L, (0.1, 0.2, 0.5), 0.0, 0.0))]
+        if three:
+            objs.append(((1.0, 0.0, -1.0), 0.5, (L, (0.8, 0.6, 0.2), 0.0, 0.0)))
+        else:
+            objs.append(((-1.0, 0.0, -1.0), 0.5, (DIELECTRIC, (0.0, 0.0, 0.0), 0.0, 1.5)))
+            objs.append(((1.0, 0.0, -1.0), 0.5, (METAL, (0.8, 0.6, 0.2), 0.0, 0.0)))
+        return cam, objs
+    if name in ("threads", "super_simple"):  # mod.rs:176-238
+        cam = Camera(pick(h, 1000), pick(w, 1000), pick(max_depth, 50), 1.0, 50.0,
+                     (0.0, 0.0, 0.0), (0.0, 0.0, -0.3), (0.0, 1.0, 0.0), 0.6, 10.0)
+        return cam, [((0.0, -100.5, -1.0), 100.0, (L, (0.8, 0.8, 0.0), 0.0, 0.0))]
+    raise ValueError(name)

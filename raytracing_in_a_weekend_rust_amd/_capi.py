@@ -123,6 +123,16 @@ class RtwError(RuntimeError):
 
 
 def _load():
+    # One HIP runtime per process. torch ships its own libamdhip64 (soname
+    # libamdhip64.so.7, requested by torch as "libamdhip64.so"). If librtw.so
+    # loaded /opt/rocm's copy first, torch would map a second runtime and find no
+    # GPU; loading torch first makes librtw.so bind to torch's copy (same soname),
+    # so torch streams and tensors are valid handles for the C ABI.
+    if os.environ.get("RTW_NO_TORCH", "0") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"librtw.so not built at {LIB_PATH}: run `make` (or __graft_entry__.build()). "

@@ -1,0 +1,99 @@
+// rtw_cli -- host driver mirroring the reference's main.rs (flags main.rs:32-87,
+// defaults main.rs:20-29) and raytracing::complex (raytracing/mod.rs:54-126):
+// builds the scene, runs Camera::threaded_render on the GPU, writes img.ppm.
+//
+// Extra flags (the reference hard-codes or time-seeds these): --depth (MAX_DEPTH,
+// mod.rs:43), --seed (both XorShift::default seeds, mod.rs:67 / camera.rs:255),
+// --scene (the other builders of mod.rs), --out. --preview is accepted and
+// ignored: the winit preview window (application/mod.rs) is out of scope.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "rtw_host.h"
+
+namespace {
+
+struct Config {  // main.rs:13-29
+    uint32_t height = 1080, width = 1920, sample_sqrt = 10, depth = 0;
+    bool preview = false;
+    std::string scene = "complex", out = "img.ppm";
+    unsigned long long seed = 0;
+    bool seed_set = false;
+};
+
+bool parse_u32(const char *s, uint32_t &v) {
+    if (!s || !*s) return false;
+    char *end = nullptr;
+    const unsigned long long x = std::strtoull(s, &end, 10);
+    if (*end || s[0] == '-' || x > 0xffffffffull) return false;
+    v = static_cast<uint32_t>(x);
+    return true;
+}
+
+Config parse_args(int argc, char **argv) {
+    Config c;
+    for (int i = 1; i < argc; ++i) {
+        const std::string a = argv[i];
+        const char *next = i + 1 < argc ? argv[i + 1] : nullptr;
+        auto need = [&](uint32_t &dst, const char *usage) {
+            if (!parse_u32(next, dst)) {
+                std::fprintf(stderr, "Usage: %s <number>\n", usage);
+                std::exit(1);
+            }
+        };
+        if (a == "--height" || a == "-h") need(c.height, "--height");
+        else if (a == "--width" || a == "-w") need(c.width, "--width");
+        else if (a == "--samplesqrt" || a == "-s") need(c.sample_sqrt, "--samplesqrt");
+        else if (a == "--depth" || a == "-d") need(c.depth, "--depth");
+        else if (a == "--preview" || a == "-p") c.preview = true;
+        else if (a == "--seed" && next) c.seed = std::strtoull(next, nullptr, 0), c.seed_set = true;
+        else if (a == "--scene" && next) c.scene = next;
+        else if (a == "--out" && next) c.out = next;
+        else if (a == "--help") {
+            std::printf("Use the application like this:\n");
+            std::printf("\t-h --height\t:\tSet the height of the image\n");
+            std::printf("\t--width -w\t:\tSet the width of the image\n");
+            std::printf("\t--samplesqrt -s\t:\tSet the sqrt of the samples used for the image\n");
+            std::printf("\t--preview -p\t:\tSet whether a preview window is displayed (ignored)\n");
+            std::printf("\t--depth -d\t:\tMax bounce depth (reference: 10)\n");
+            std::printf("\t--seed N\t:\tXorShift seed for scene and render (reference: wall-clock ms)\n");
+            std::printf("\t--scene NAME\t:\tcomplex | simple | threads | super_simple | three_lambertian\n");
+            std::printf("\t--out PATH\t:\tOutput PPM (reference: img.ppm)\n");
+            std::exit(0);
+        }
+    }
+    if (!c.seed_set)  // XorShift::default(): milliseconds since the Unix epoch
+        c.seed = static_cast<unsigned long long>(
+            std::chrono::duration_cast<std::chrono::milliseconds>(
+                std::chrono::system_clock::now().time_since_epoch())
+                .count());
+    return c;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const Config cfg = parse_args(argc, argv);
+    if (cfg.preview) std::fprintf(stderr, "note: --preview is not supported; rendering headless\n");
+    try {
+        const rtw_u128 seed{cfg.seed, 0};
+        rtw::BuiltScene b = rtw::build_scene(cfg.scene, seed, cfg.height, cfg.width, cfg.depth);
+        std::printf(
+            "\n            Multithreaded rendering\n            Making an image of format:\n"
+            "                %u by %u\n                %u samples\n                %u max depth\n\n",
+            b.cam.width(), b.cam.height(), cfg.sample_sqrt * cfg.sample_sqrt, b.cam.d.max_depth);
+        rtw_stats st{};
+        const auto t0 = std::chrono::steady_clock::now();
+        rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("Finished succesfully: %s (%.3f s wall, kernel %.3f ms, %.1f Msamples/s, seed %llu)\n",
+                    cfg.out.c_str(), s, st.kernel_ms, st.samples / st.kernel_ms / 1e3, cfg.seed);
+    } catch (const rtw::Error &e) {
+        std::fprintf(stderr, "\nRender thread errored with %s\n", e.what());
+        return 1;
+    }
+    return 0;
+}

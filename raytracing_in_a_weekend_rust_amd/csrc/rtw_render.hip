@@ -23,7 +23,9 @@
 // per-lane stack of material indices, so it associates exactly as the recursion.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -37,7 +39,14 @@ namespace {
 
 constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 constexpr int kTile = 16;
-constexpr uint32_t kLdsSphereCap = 2048;  // 64 KiB of {cx,cy,cz,r*r}
+constexpr uint32_t kLdsSphereCap = 1024;  // 52 B/sphere staged: <= 52 KiB of LDS
+constexpr int kChunk = 64;                // spheres per candidate mask (one bit per sphere)
+
+// Conservative f32 pre-filter for Sphere::hit's discriminant (see filter_margin
+// below). K1 = 2^-15 = 512 u32; the first-order bound needs 140 u32.
+constexpr float kFilterK1 = 3.0517578125e-05f;  // 2^-15
+constexpr float kFilterFloor = 1e-25f;          // covers f32 underflow within the guard
+constexpr double kGuardLo = 1e-12, kGuardHi = 1e12;
 
 struct U128 {
     uint64_t lo, hi;
@@ -51,7 +60,9 @@ struct KParams {
     uint32_t row_begin, row_step, n_rows, n_sph;
     uint32_t jump_bits, _pad;
     uint64_t seed_lo, seed_hi;
-    const double4 *sph;         // {cx, cy, cz, r*r}
+    const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
+    const float4 *sph32;        // {cx, cy, cz, r*r} rounded to f32 (filter only)
+    const float *sphw;          // filter weight W_s >= m_c^2 + r*r/2 (rounded up; inf = always test)
     const double *radius;       // r
     const uint32_t *sph_mat;    // material row per sphere
     const rtw_material *mats;   // material table
@@ -140,13 +151,25 @@ __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &u
 }
 
 // ---------------------------------------------------------------- megakernel --
-template <int CAP, bool kLds>
+template <bool kLds, bool kFilter>
 __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
-    extern __shared__ double4 lds_sph[];
-    const double4 *__restrict__ sph = kLds ? lds_sph : P.sph;
+    // LDS: [n x double4 exact spheres][n x float4 filter spheres][n x float weights]
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    const uint32_t n = P.n_sph;
+    const double4 *__restrict__ sph = P.sph;
+    const float4 *__restrict__ sph32 = P.sph32;
+    const float *__restrict__ sphw = P.sphw;
     if (kLds) {
-        for (uint32_t i = threadIdx.x; i < P.n_sph; i += kBlock) lds_sph[i] = P.sph[i];
+        double4 *l64 = reinterpret_cast<double4 *>(lds_raw);
+        float4 *l32 = reinterpret_cast<float4 *>(lds_raw + static_cast<size_t>(n) * sizeof(double4));
+        float *lw = reinterpret_cast<float *>(lds_raw + static_cast<size_t>(n) * (sizeof(double4) + sizeof(float4)));
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+            l64[i] = P.sph[i];
+            l32[i] = P.sph32[i];
+            lw[i] = P.sphw[i];
+        }
         __syncthreads();
+        sph = l64, sph32 = l32, sphw = lw;
     }
 
     const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
@@ -198,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         if (P.max_depth == 0) {  // every sample is black, RNG still consumed by get_ray
             for (uint32_t k = 0; k < n_off; ++k) gen_ray(k);
         } else {
-            uint16_t stk[CAP];
+            uint16_t stk[1024];  // material rows of the path's non-dielectric bounces (scratch)
             uint32_t nst = 0, depth = 0, k = 0;
             gen_ray(0);
             for (;;) {
@@ -207,19 +230,66 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                 const double a = dx * dx + dy * dy + dz * dz;
                 int best = -1;
                 double bt = 0.;
-                for (uint32_t i = 0; i < P.n_sph; ++i) {
-                    const double4 S = sph[i];
-                    const double ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
-                    const double hb = ocx * dx + ocy * dy + ocz * dz;
-                    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - S.w;
-                    const double disc = hb * hb - a * c;
-                    if (!(disc < 0.)) {
-                        const double sq = __builtin_sqrt(disc);
-                        double t = (-sq - hb) / a;
-                        if (!(t >= 0.01)) t = (sq - hb) / a;
-                        if (t >= 0.01 && (best < 0 || t < bt)) {
-                            bt = t;
-                            best = static_cast<int>(i);
+
+                // Filter setup. The f32 pass may only be used inside the guard
+                // (no f32 overflow, underflow errors below kFilterFloor).
+                const double mo64 = fmax(fmax(__builtin_fabs(ox), __builtin_fabs(oy)), __builtin_fabs(oz));
+                const bool fast = kFilter && a >= kGuardLo && a <= kGuardHi && mo64 <= kGuardHi;
+                const float o32x = static_cast<float>(ox), o32y = static_cast<float>(oy),
+                            o32z = static_cast<float>(oz);
+                const float d32x = static_cast<float>(dx), d32y = static_cast<float>(dy),
+                            d32z = static_cast<float>(dz);
+                const float a32 = static_cast<float>(a);
+                const float mo = static_cast<float>(mo64) * 1.00000095367431640625f;  // (1 + 2^-20): round up
+                const float H = a32 * kFilterK1;
+                const float G = fmaf(H * mo, mo, kFilterFloor);
+
+                for (uint32_t base = 0; base < n; base += kChunk) {
+                    const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
+                    uint64_t mask;
+                    if (fast) {
+                        // Pass 1 (f32, FMA): candidate unless the discriminant is
+                        // provably negative. With oc, d, a, r*r rounded to f32 and
+                        // M_i = |o_i| + |c_i| <= m_o + m_c, a first-order bound is
+                        //   |D32 - D| <= u32 * a * (70 M^2 + 7 r*r)
+                        //              <= 140 u32 * a * (m_o^2 + m_c^2 + r*r/2)
+                        // (D the exact real discriminant; the f64 reference value is
+                        // within 1e-14 of that). margin = 512 u32 * a * (m_o^2 + W_s)
+                        // + floor, so every sphere whose f64 discriminant is >= 0
+                        // (or NaN) is kept. Derivation: DESIGN.md, "Exact pre-filter".
+                        mask = 0;
+#pragma unroll 4
+                        for (uint32_t j = 0; j < cnt; ++j) {
+                            const float4 S = sph32[base + j];
+                            const float w = sphw[base + j];
+                            const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
+                            const float hb = fmaf(ocx, d32x, fmaf(ocy, d32y, ocz * d32z));
+                            const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+                            const float disc = fmaf(hb, hb, -(a32 * c));
+                            const float margin = fmaf(H, w, G);
+                            if (!(disc < -margin)) mask |= 1ull << j;
+                        }
+                    } else {
+                        mask = cnt == 64u ? ~0ull : ((1ull << cnt) - 1ull);
+                    }
+                    // Pass 2 (f64, exactly sphere.rs:39-71) on this lane's
+                    // candidates, in index order.
+                    while (mask) {
+                        const uint32_t i = base + static_cast<uint32_t>(__builtin_ctzll(mask));
+                        mask &= mask - 1ull;
+                        const double4 S = sph[i];
+                        const double ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
+                        const double hb = ocx * dx + ocy * dy + ocz * dz;
+                        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - S.w;
+                        const double disc = hb * hb - a * c;
+                        if (!(disc < 0.)) {
+                            const double sq = __builtin_sqrt(disc);
+                            double t = (-sq - hb) / a;
+                            if (!(t >= 0.01)) t = (sq - hb) / a;
+                            if (t >= 0.01 && (best < 0 || t < bt)) {
+                                bt = t;
+                                best = static_cast<int>(i);
+                            }
                         }
                     }
                 }
@@ -360,6 +430,8 @@ struct rtw_session {
     int device = 0;
     hipStream_t own = nullptr;
     double4 *d_sph = nullptr;
+    float4 *d_sph32 = nullptr;
+    float *d_sphw = nullptr;
     double *d_rad = nullptr;
     uint32_t *d_smat = nullptr;
     rtw_material *d_mats = nullptr;
@@ -403,25 +475,47 @@ void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uin
         if (sp[i].mat >= nm) throw rtw::Error(RTW_E_MAT_INDEX, "sphere material index out of range");
 }
 
+// f32 value >= x (x finite, >= 0): round to nearest, then one ulp up.
+float round_up_f32(double x) {
+    if (!(x >= 0.) || !(x <= 1e36)) return INFINITY;
+    return std::nextafter(static_cast<float>(x), INFINITY);
+}
+
 void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
-    dev_free(s->d_sph), dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
-    s->d_sph = nullptr, s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
+    dev_free(s->d_sph), dev_free(s->d_sph32), dev_free(s->d_sphw);
+    dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    s->d_sph = nullptr, s->d_sph32 = nullptr, s->d_sphw = nullptr;
+    s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
     std::vector<double4> a(n ? n : 1);
+    std::vector<float4> a32(n ? n : 1);
+    std::vector<float> w(n ? n : 1);
     std::vector<double> r(n ? n : 1);
     std::vector<uint32_t> mi(n ? n : 1);
     for (uint32_t i = 0; i < n; ++i) {
         const double rad = sp[i].radius;
-        a[i] = make_double4(sp[i].center[0], sp[i].center[1], sp[i].center[2], rad * rad);
+        const double rr = rad * rad;  // sphere.rs:49 `self.radius * self.radius`
+        const double *c = sp[i].center;
+        a[i] = make_double4(c[0], c[1], c[2], rr);
+        a32[i] = make_float4(static_cast<float>(c[0]), static_cast<float>(c[1]),
+                             static_cast<float>(c[2]), static_cast<float>(rr));
+        // filter weight W_s >= m_c^2 + r*r/2, m_c = max |c_i|; spheres outside the
+        // guard (|c| > 1e12, non-finite) get +inf: always tested exactly.
+        const double mc = std::fmax(std::fmax(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2]));
+        w[i] = (mc <= kGuardHi && std::isfinite(rr)) ? round_up_f32(mc * mc + rr / 2.) : INFINITY;
         r[i] = rad;
         mi[i] = sp[i].mat;
     }
     HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
+    HIPCHECK(hipMalloc(&s->d_sph32, a32.size() * sizeof(float4)));
+    HIPCHECK(hipMalloc(&s->d_sphw, w.size() * sizeof(float)));
     HIPCHECK(hipMalloc(&s->d_rad, r.size() * sizeof(double)));
     HIPCHECK(hipMalloc(&s->d_smat, mi.size() * sizeof(uint32_t)));
     HIPCHECK(hipMalloc(&s->d_mats, (nm ? nm : 1) * sizeof(rtw_material)));
     HIPCHECK(hipMemcpy(s->d_sph, a.data(), a.size() * sizeof(double4), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_sph32, a32.data(), a32.size() * sizeof(float4), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_sphw, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_rad, r.data(), r.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_smat, mi.data(), mi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     if (nm) HIPCHECK(hipMemcpy(s->d_mats, m, nm * sizeof(rtw_material), hipMemcpyHostToDevice));
@@ -488,6 +582,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.seed_lo = seed.lo;
     P.seed_hi = seed.hi;
     P.sph = s->d_sph;
+    P.sph32 = s->d_sph32;
+    P.sphw = s->d_sphw;
     P.radius = s->d_rad;
     P.sph_mat = s->d_smat;
     P.mats = s->d_mats;
@@ -496,20 +592,19 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.counters = s->d_counters;
 
     HIPCHECK(hipSetDevice(s->device));
-    hipStream_t st = stream ? stream : s->own;
+    hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
     const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
     const bool use_lds = P.n_sph <= kLdsSphereCap;
-    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * sizeof(double4) : 0;
+    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * (sizeof(double4) + sizeof(float4) + sizeof(float)) : 0;
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, 2 * sizeof(unsigned long long), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     if (P.n_rows) {
-        if (P.max_depth <= 64) {
-            if (use_lds) hipLaunchKernelGGL((rtw_render_f64<64, true>), grid, dim3(kBlock), lds, st, P);
-            else hipLaunchKernelGGL((rtw_render_f64<64, false>), grid, dim3(kBlock), 0, st, P);
-        } else {
-            if (use_lds) hipLaunchKernelGGL((rtw_render_f64<1024, true>), grid, dim3(kBlock), lds, st, P);
-            else hipLaunchKernelGGL((rtw_render_f64<1024, false>), grid, dim3(kBlock), 0, st, P);
-        }
+        const char *fenv = std::getenv("RTW_FILTER");  // 0 = brute-force f64 scan (A/B, tests)
+        const bool filt = fenv ? std::atoi(fenv) != 0 : true;
+        if (use_lds && filt) hipLaunchKernelGGL((rtw_render_f64<true, true>), grid, dim3(kBlock), lds, st, P);
+        else if (use_lds) hipLaunchKernelGGL((rtw_render_f64<true, false>), grid, dim3(kBlock), lds, st, P);
+        else if (filt) hipLaunchKernelGGL((rtw_render_f64<false, true>), grid, dim3(kBlock), 0, st, P);
+        else hipLaunchKernelGGL((rtw_render_f64<false, false>), grid, dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
     }
     HIPCHECK(hipEventRecord(s->ev1, st));
@@ -598,7 +693,8 @@ int rtw_session_destroy(rtw_session *s) {
     if (!s) return RTW_OK;
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
-    dev_free(s->d_sph), dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    dev_free(s->d_sph), dev_free(s->d_sph32), dev_free(s->d_sphw);
+    dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
     dev_free(s->d_jump), dev_free(s->d_counters);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -654,7 +750,7 @@ int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32
     set_scene(cached, spheres, n_spheres, mats, n_mats);
     const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(double);
     HIPCHECK(hipMalloc(&d_out, bytes ? bytes : 8));
-    render(cached, cam, samples_sqrt, seed, &sh, d_out, nullptr);
+    render(cached, cam, samples_sqrt, seed, &sh, d_out, cached->own);
     collect(cached);
     if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
     HIPCHECK(hipFree(d_out));
