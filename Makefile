@@ -32,6 +32,13 @@ $(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
 oracle:
 	$(MAKE) -C oracle
 
+# diagnostic build with per-wave s_memtime section stamps (tools/stamps.py)
+stamps: $(OUT)/librtw_stamps.so
+$(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
+	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
+$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_host.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
+
 asm: $(SRC)/rtw_render.hip
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/rtw_render.s $<
@@ -40,4 +47,4 @@ clean:
 	rm -rf $(OUT) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean
+.PHONY: all oracle asm clean stamps

@@ -179,7 +179,9 @@ def main():
                                  "filter, so peak = FP32 vector; frac vs FP64 vector peak = "
                                  f"{achieved / FP64_VECTOR_PEAK:.4f}"},
             "stats": {"segments": st.segments, "segments_per_sample": round(st.segments / max(1, st.samples), 4),
-                      "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4)},
+                      "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
+                      "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
+                      "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3)},
         }
     if rank == 0 and world == 1 and a.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "librtw.so")
+LIB_PATH = os.environ.get("RTW_LIB") or os.path.join(_HERE, "_lib", "librtw.so")
 
 
 class Vec3(C.Structure):
@@ -67,6 +67,7 @@ class Shard(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("pixels", C.c_uint64), ("samples", C.c_uint64), ("segments", C.c_uint64),
                 ("sphere_tests", C.c_uint64), ("wave_iterations", C.c_uint64),
+                ("exact_tests", C.c_uint64), ("exact_wave_iterations", C.c_uint64),
                 ("kernel_ms", C.c_double), ("grid_blocks", C.c_uint32),
                 ("block_threads", C.c_uint32)]
 

@@ -39,14 +39,28 @@ namespace {
 
 constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 constexpr int kTile = 16;
-constexpr uint32_t kLdsSphereCap = 1024;  // 52 B/sphere staged: <= 52 KiB of LDS
-constexpr int kChunk = 64;                // spheres per candidate mask (one bit per sphere)
+constexpr uint32_t kLdsSphereCap = 2048;  // exact f64 records staged in LDS: <= 64 KiB
+constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
+constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 
-// Conservative f32 pre-filter for Sphere::hit's discriminant (see filter_margin
-// below). K1 = 2^-15 = 512 u32; the first-order bound needs 140 u32.
-constexpr float kFilterK1 = 3.0517578125e-05f;  // 2^-15
-constexpr float kFilterFloor = 1e-25f;          // covers f32 underflow within the guard
-constexpr double kGuardLo = 1e-12, kGuardHi = 1e12;
+// Exact-conservative f32 pre-filter of Sphere::hit's discriminant (derivation in
+// the pass-1 comment and DESIGN.md "Exact pre-filter"). K = 2^-15 = 512 u32; the
+// first-order error bound needs 163 u32.
+constexpr double kFilterK = 3.0517578125e-05;   // 2^-15
+constexpr double kFilterFloor = 1e-25;          // f32 underflow errors inside the guard
+constexpr double kGuardHi = 1e12;               // max |origin| component for the f32 pass
+
+// Wave-uniform load of a pass-1 record through the constant address space, so the
+// compiler emits s_load (4 records per s_load_dwordx16) and feeds SGPR operands.
+__device__ __forceinline__ float4 ld_filt(const float4 *p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) float cfloat;
+    const cfloat *q = (const cfloat *)(p);
+    return make_float4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+#else
+    return p[i];
+#endif
+}
 
 struct U128 {
     uint64_t lo, hi;
@@ -61,14 +75,15 @@ struct KParams {
     uint32_t jump_bits, _pad;
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
-    const float4 *sph32;        // {cx, cy, cz, r*r} rounded to f32 (filter only)
-    const float *sphw;          // filter weight W_s >= m_c^2 + r*r/2 (rounded up; inf = always test)
+    const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
     const double *radius;       // r
     const uint32_t *sph_mat;    // material row per sphere
     const rtw_material *mats;   // material table
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
-    unsigned long long *counters;  // [0] segments, [1] wave iterations
+    uint16_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
+    uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
+    unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests, [3] wave exact-pass iterations
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -150,31 +165,73 @@ __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &u
     uz = z / l;
 }
 
+// Material rows of the current path's non-dielectric bounces (dielectric
+// attenuation is (1,1,1): an exact no-op in the product). The first kRegSlots
+// entries live in two u64 registers; deeper ones go to a coalesced HBM buffer
+// (one u16 per pixel per level). No private/scratch memory is used: a scratch
+// array caps the waves a CU may hold.
+constexpr uint32_t kRegSlots = 8;
+struct PathStack {
+    uint64_t r0 = 0, r1 = 0;
+    uint32_t n = 0;
+    __device__ __forceinline__ void push(uint32_t v, uint16_t *spill, uint64_t stride, uint64_t pix) {
+        if (n < 4) r0 |= static_cast<uint64_t>(v) << (16u * n);
+        else if (n < kRegSlots) r1 |= static_cast<uint64_t>(v) << (16u * (n - 4u));
+        else spill[static_cast<uint64_t>(n - kRegSlots) * stride + pix] = static_cast<uint16_t>(v);
+        ++n;
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t j, const uint16_t *spill, uint64_t stride,
+                                           uint64_t pix) const {
+        if (j < 4) return static_cast<uint32_t>(r0 >> (16u * j)) & 0xffffu;
+        if (j < kRegSlots) return static_cast<uint32_t>(r1 >> (16u * (j - 4u))) & 0xffffu;
+        return spill[static_cast<uint64_t>(j - kRegSlots) * stride + pix];
+    }
+    __device__ __forceinline__ void clear() { r0 = r1 = 0, n = 0; }
+};
+
+// Diagnostic build only (-DRTW_STAMPS, librtw_stamps.so): per-wave s_memtime
+// cycle sums per section; never compiled into the product library.
+#ifdef RTW_STAMPS
+#define STAMP_DECL uint64_t st_last = stamp_now(), st_acc[6] = {0, 0, 0, 0, 0, 0};
+#define STAMP(k)                                   \
+    do {                                           \
+        const uint64_t t_ = stamp_now();           \
+        st_acc[k] += t_ - st_last;                 \
+        st_last = t_;                              \
+    } while (0)
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+#define STAMP_DECL
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------- megakernel --
 template <bool kLds, bool kFilter>
 __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
-    // LDS: [n x double4 exact spheres][n x float4 filter spheres][n x float weights]
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    // LDS: exact f64 sphere records for the per-lane candidate pass.
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const uint32_t n = P.n_sph;
     const double4 *__restrict__ sph = P.sph;
-    const float4 *__restrict__ sph32 = P.sph32;
-    const float *__restrict__ sphw = P.sphw;
     if (kLds) {
-        double4 *l64 = reinterpret_cast<double4 *>(lds_raw);
-        float4 *l32 = reinterpret_cast<float4 *>(lds_raw + static_cast<size_t>(n) * sizeof(double4));
-        float *lw = reinterpret_cast<float *>(lds_raw + static_cast<size_t>(n) * (sizeof(double4) + sizeof(float4)));
-        for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-            l64[i] = P.sph[i];
-            l32[i] = P.sph32[i];
-            lw[i] = P.sphw[i];
-        }
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock) lds_sph[i] = P.sph[i];
         __syncthreads();
-        sph = l64, sph32 = l32, sphw = lw;
+        sph = lds_sph;
     }
+    const float4 *filt = P.filt;
 
     const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
     const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
-    uint32_t seg = 0;
+    uint32_t seg = 0, ntest = 0, nwave2 = 0;
+    const uint32_t lane = threadIdx.x & 63u;
+    STAMP_DECL
 
     if (x < P.W && lr < P.n_rows) {
         const uint32_t y = P.row_begin + lr * P.row_step;
@@ -221,9 +278,12 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         if (P.max_depth == 0) {  // every sample is black, RNG still consumed by get_ray
             for (uint32_t k = 0; k < n_off; ++k) gen_ray(k);
         } else {
-            uint16_t stk[1024];  // material rows of the path's non-dielectric bounces (scratch)
-            uint32_t nst = 0, depth = 0, k = 0;
+            PathStack stk;
+            const uint64_t pix = static_cast<uint64_t>(lr) * P.W + x;  // spill column
+            const uint64_t stride = static_cast<uint64_t>(P.n_rows) * P.W;
+            uint32_t depth = 0, k = 0;
             gen_ray(0);
+            STAMP(0);  // 0: seed jump + pixel setup
             for (;;) {
                 // ---- Scene::hit: all spheres, first minimum wins ----
                 ++seg;
@@ -231,52 +291,59 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                 int best = -1;
                 double bt = 0.;
 
-                // Filter setup. The f32 pass may only be used inside the guard
-                // (no f32 overflow, underflow errors below kFilterFloor).
+                // ---- pass 1 setup: f32 unit direction e, per-lane margin G ----
+                // Exact-conservative filter. With ê = d/|d| the discriminant's sign is
+                // that of D' = (OC.ê)^2 - (|OC|^2 - R2) = D / a. Computed in f32 with
+                // oc = o32 - c32, e = fl32(ê), and R2' >= R2 + K (m_c^2 + R2/2) in
+                // place of R2 (host, rounded up), a first-order bound of the f32
+                // error is  u32 (81 M^2 + 4 R2') with M_i = |o_i| + |c_i|,
+                // M^2 <= 2 (m_o^2 + m_c^2); K = 512 u32 then leaves
+                //   disc32 >= D' - K m_o^2 - (floor)
+                // so every sphere whose f64 discriminant is >= 0 (or NaN) passes the
+                // test disc32 >= -G, G = K m_o^2 + floor. NaN/inf anywhere -> kept.
                 const double mo64 = fmax(fmax(__builtin_fabs(ox), __builtin_fabs(oy)), __builtin_fabs(oz));
-                const bool fast = kFilter && a >= kGuardLo && a <= kGuardHi && mo64 <= kGuardHi;
+                const bool fast = kFilter && mo64 <= kGuardHi;  // false for NaN too
+                const double inv = 1.0 / __builtin_sqrt(a);
+                const float ex = static_cast<float>(dx * inv), ey = static_cast<float>(dy * inv),
+                            ez = static_cast<float>(dz * inv);
                 const float o32x = static_cast<float>(ox), o32y = static_cast<float>(oy),
                             o32z = static_cast<float>(oz);
-                const float d32x = static_cast<float>(dx), d32y = static_cast<float>(dy),
-                            d32z = static_cast<float>(dz);
-                const float a32 = static_cast<float>(a);
-                const float mo = static_cast<float>(mo64) * 1.00000095367431640625f;  // (1 + 2^-20): round up
-                const float H = a32 * kFilterK1;
-                const float G = fmaf(H * mo, mo, kFilterFloor);
+                const float negG = -static_cast<float>(fma(kFilterK * mo64, mo64 * 1.000001, kFilterFloor));
 
+                STAMP(5);  // 5: segment setup
                 for (uint32_t base = 0; base < n; base += kChunk) {
                     const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
-                    uint64_t mask;
+                    // sphere base+j is bit (31 - j): highest set bit = lowest index
+                    uint32_t mask;
                     if (fast) {
-                        // Pass 1 (f32, FMA): candidate unless the discriminant is
-                        // provably negative. With oc, d, a, r*r rounded to f32 and
-                        // M_i = |o_i| + |c_i| <= m_o + m_c, a first-order bound is
-                        //   |D32 - D| <= u32 * a * (70 M^2 + 7 r*r)
-                        //              <= 140 u32 * a * (m_o^2 + m_c^2 + r*r/2)
-                        // (D the exact real discriminant; the f64 reference value is
-                        // within 1e-14 of that). margin = 512 u32 * a * (m_o^2 + W_s)
-                        // + floor, so every sphere whose f64 discriminant is >= 0
-                        // (or NaN) is kept. Derivation: DESIGN.md, "Exact pre-filter".
                         mask = 0;
-#pragma unroll 4
-                        for (uint32_t j = 0; j < cnt; ++j) {
-                            const float4 S = sph32[base + j];
-                            const float w = sphw[base + j];
-                            const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
-                            const float hb = fmaf(ocx, d32x, fmaf(ocy, d32y, ocz * d32z));
-                            const float c = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-                            const float disc = fmaf(hb, hb, -(a32 * c));
-                            const float margin = fmaf(H, w, G);
-                            if (!(disc < -margin)) mask |= 1ull << j;
+                        for (uint32_t g = 0; g < static_cast<uint32_t>(kChunk); g += kGroup) {
+#pragma unroll
+                            for (int j = 0; j < kGroup; ++j) {
+                                const float4 S = ld_filt(filt, base + g + j);  // wave-uniform: s_load
+                                const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
+                                const float hb = fmaf(ocx, ex, fmaf(ocy, ey, ocz * ez));
+                                const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+                                const float disc = fmaf(hb, hb, -cc);
+                                mask = mask + mask + static_cast<uint32_t>(!(disc < negG));
+                            }
                         }
+                        if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
                     } else {
-                        mask = cnt == 64u ? ~0ull : ((1ull << cnt) - 1ull);
+                        mask = cnt == static_cast<uint32_t>(kChunk) ? ~0u : ~((1u << (kChunk - cnt)) - 1u);
                     }
+                    STAMP(1);  // 1: pass 1 (f32 filter)
                     // Pass 2 (f64, exactly sphere.rs:39-71) on this lane's
                     // candidates, in index order.
                     while (mask) {
-                        const uint32_t i = base + static_cast<uint32_t>(__builtin_ctzll(mask));
-                        mask &= mask - 1ull;
+                        ++ntest;
+                        {  // the wave's first active lane counts the wave-level iteration
+                            const uint64_t exm = __builtin_amdgcn_read_exec();
+                            nwave2 += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
+                        }
+                        const uint32_t top = 31u - static_cast<uint32_t>(__builtin_clz(mask));
+                        mask ^= 1u << top;
+                        const uint32_t i = base + (31u - top);
                         const double4 S = sph[i];
                         const double ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
                         const double hb = ocx * dx + ocy * dy + ocz * dz;
@@ -292,6 +359,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                             }
                         }
                     }
+                    STAMP(2);  // 2: pass 2 (exact f64 tests)
                 }
 
                 bool finish;
@@ -312,7 +380,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                         random_unit_vec(rng, ux, uy, uz);
                         ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
                         if (ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = nx, ndy = ny, ndz = nz;
-                        stk[nst++] = static_cast<uint16_t>(mi);
+                        stk.push(mi, P.spill, stride, pix);
                     } else if (M.kind == RTW_METAL) {  // materials.rs:52-63
                         const double l = __builtin_sqrt(a);
                         const double vx = dx / l, vy = dy / l, vz = dz / l;
@@ -322,7 +390,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                         double ux, uy, uz;
                         random_unit_vec(rng, ux, uy, uz);
                         ndx = rx + ux * M.fuzz, ndy = ry + uy * M.fuzz, ndz = rz + uz * M.fuzz;
-                        stk[nst++] = static_cast<uint16_t>(mi);
+                        stk.push(mi, P.spill, stride, pix);
                     } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
                         const double ratio = front ? 1. / M.ir : M.ir;
                         const double l = __builtin_sqrt(a);
@@ -365,19 +433,22 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                     finish = true;
                 }
 
+                STAMP(3);  // 3: hit record + scatter / sky
                 if (finish) {
                     // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion
-                    while (nst > 0) {
-                        const rtw_material &A = P.mats[stk[--nst]];
+                    for (uint32_t j = stk.n; j-- > 0;) {
+                        const rtw_material &A = P.mats[stk.at(j, P.spill, stride, pix)];
                         lr_ = A.albedo[0] * lr_;
                         lg = A.albedo[1] * lg;
                         lb = A.albedo[2] * lb;
                     }
+                    stk.clear();
                     accr = accr + lr_, accg = accg + lg, accb = accb + lb;
                     if (++k >= n_off) break;
                     depth = 0;
                     gen_ray(k);
                 }
+                STAMP(4);  // 4: fold + next sample
             }
         }
         const double nf = static_cast<double>(n_off);
@@ -388,11 +459,32 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
     }
 
     // segments (atomic, wave-reduced by the compiler) and the wave's trip count
+#ifdef RTW_STAMPS
+    {  // max over lanes of each section sum -> one row per wave
+        uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.y) * gridDim.x * 4 + blockIdx.x * 4 + threadIdx.x / 64u) * 8;
+        for (int k = 0; k < 6; ++k) {
+            uint64_t v = st_acc[k];
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint64_t o = __shfl_xor(v, off);
+                v = v > o ? v : o;
+            }
+            if (lane == 0) row[k] = v;
+        }
+        uint64_t sm = seg;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(sm, off);
+            sm = sm > o ? sm : o;
+        }
+        if (lane == 0) row[6] = sm, row[7] = stamp_now();
+    }
+#endif
     if (P.counters) {
         if (seg) atomicAdd(&P.counters[0], static_cast<unsigned long long>(seg));
         uint32_t m = seg;
         for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&P.counters[1], static_cast<unsigned long long>(m));
+        if (ntest) atomicAdd(&P.counters[2], static_cast<unsigned long long>(ntest));
+        if (nwave2) atomicAdd(&P.counters[3], static_cast<unsigned long long>(nwave2));
     }
 }
 
@@ -430,13 +522,14 @@ struct rtw_session {
     int device = 0;
     hipStream_t own = nullptr;
     double4 *d_sph = nullptr;
-    float4 *d_sph32 = nullptr;
-    float *d_sphw = nullptr;
+    float4 *d_filt = nullptr;
     double *d_rad = nullptr;
     uint32_t *d_smat = nullptr;
     rtw_material *d_mats = nullptr;
     uint4 *d_jump = nullptr;
     unsigned long long *d_counters = nullptr;
+    uint16_t *d_spill = nullptr;
+    size_t spill_bytes = 0;
     uint32_t n_sph = 0, n_mats = 0;
     bool scene_set = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -484,13 +577,14 @@ float round_up_f32(double x) {
 void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
-    dev_free(s->d_sph), dev_free(s->d_sph32), dev_free(s->d_sphw);
+    dev_free(s->d_sph), dev_free(s->d_filt);
     dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
-    s->d_sph = nullptr, s->d_sph32 = nullptr, s->d_sphw = nullptr;
+    s->d_sph = nullptr, s->d_filt = nullptr;
     s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
+    const uint32_t npad = (n + kChunk - 1) / kChunk * kChunk;
     std::vector<double4> a(n ? n : 1);
-    std::vector<float4> a32(n ? n : 1);
-    std::vector<float> w(n ? n : 1);
+    // padding records can never be candidates (R2' = -inf -> disc = -inf)
+    std::vector<float4> f(npad ? npad : kChunk, make_float4(0.f, 0.f, 0.f, -INFINITY));
     std::vector<double> r(n ? n : 1);
     std::vector<uint32_t> mi(n ? n : 1);
     for (uint32_t i = 0; i < n; ++i) {
@@ -498,24 +592,24 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         const double rr = rad * rad;  // sphere.rs:49 `self.radius * self.radius`
         const double *c = sp[i].center;
         a[i] = make_double4(c[0], c[1], c[2], rr);
-        a32[i] = make_float4(static_cast<float>(c[0]), static_cast<float>(c[1]),
-                             static_cast<float>(c[2]), static_cast<float>(rr));
-        // filter weight W_s >= m_c^2 + r*r/2, m_c = max |c_i|; spheres outside the
-        // guard (|c| > 1e12, non-finite) get +inf: always tested exactly.
+        // R2' >= r*r + K (m_c^2 + r*r/2), m_c = max |c_i|, rounded up to f32; +inf
+        // (always tested exactly) outside the guard or for non-finite input.
         const double mc = std::fmax(std::fmax(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2]));
-        w[i] = (mc <= kGuardHi && std::isfinite(rr)) ? round_up_f32(mc * mc + rr / 2.) : INFINITY;
+        const float r2p = (mc <= kGuardHi && std::isfinite(rr))
+                              ? round_up_f32(rr + kFilterK * (mc * mc + rr / 2.) * (1. + 1e-6))
+                              : INFINITY;
+        f[i] = make_float4(static_cast<float>(c[0]), static_cast<float>(c[1]),
+                           static_cast<float>(c[2]), r2p);
         r[i] = rad;
         mi[i] = sp[i].mat;
     }
     HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
-    HIPCHECK(hipMalloc(&s->d_sph32, a32.size() * sizeof(float4)));
-    HIPCHECK(hipMalloc(&s->d_sphw, w.size() * sizeof(float)));
+    HIPCHECK(hipMalloc(&s->d_filt, f.size() * sizeof(float4)));
     HIPCHECK(hipMalloc(&s->d_rad, r.size() * sizeof(double)));
     HIPCHECK(hipMalloc(&s->d_smat, mi.size() * sizeof(uint32_t)));
     HIPCHECK(hipMalloc(&s->d_mats, (nm ? nm : 1) * sizeof(rtw_material)));
     HIPCHECK(hipMemcpy(s->d_sph, a.data(), a.size() * sizeof(double4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_sph32, a32.data(), a32.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_sphw, w.data(), w.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_filt, f.data(), f.size() * sizeof(float4), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_rad, r.data(), r.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_smat, mi.data(), mi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     if (nm) HIPCHECK(hipMemcpy(s->d_mats, m, nm * sizeof(rtw_material), hipMemcpyHostToDevice));
@@ -537,13 +631,17 @@ rtw_shard resolve_shard(const rtw_camera *cam, const rtw_shard *shard) {
     return sh;
 }
 
+#ifdef RTW_STAMPS
+uint64_t *&stamp_buf() { static uint64_t *p = nullptr; return p; }
+size_t &stamp_n() { static size_t n = 0; return n; }
+#endif
+
 void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
             const rtw_shard *shard_in, double *out, hipStream_t stream) {
     if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
     if (!s->scene_set) throw rtw::Error(RTW_E_ARG, "session has no scene");
     if (cam->img_height == 0 || cam->img_width == 0)
         throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");  // camera.rs:267
-    if (cam->max_depth > 1024) throw rtw::Error(RTW_E_UNSUPPORTED, "max_depth > 1024");
     if (samples_sqrt > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "samples_sqrt > 65535");
     const uint64_t npix = static_cast<uint64_t>(cam->img_height) * cam->img_width;
     const uint32_t bits = bit_length(npix - 1);
@@ -582,21 +680,50 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.seed_lo = seed.lo;
     P.seed_hi = seed.hi;
     P.sph = s->d_sph;
-    P.sph32 = s->d_sph32;
-    P.sphw = s->d_sphw;
+    P.filt = s->d_filt;
     P.radius = s->d_rad;
     P.sph_mat = s->d_smat;
     P.mats = s->d_mats;
     P.jump = s->d_jump;
     P.out = out;
+    // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
+    const size_t spill_need = cam->max_depth > kRegSlots
+                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint16_t)
+                                  : 0;
+    if (spill_need > s->spill_bytes) {
+        HIPCHECK(hipSetDevice(s->device));
+        HIPCHECK(hipStreamSynchronize(stream ? stream : nullptr));
+        if (s->pending) HIPCHECK(hipEventSynchronize(s->ev1));
+        dev_free(s->d_spill);
+        s->d_spill = nullptr, s->spill_bytes = 0;
+        HIPCHECK(hipMalloc(&s->d_spill, spill_need));
+        s->spill_bytes = spill_need;
+    }
+    P.spill = s->d_spill;
+#ifdef RTW_STAMPS
+    {
+        const size_t nw = static_cast<size_t>((P.W + kTile - 1) / kTile) * ((sh.n_rows + kTile - 1) / kTile) * 4;
+        static uint64_t *d_st = nullptr;
+        static size_t cap = 0;
+        if (nw * 64 > cap) {
+            if (d_st) (void)hipFree(d_st);
+            HIPCHECK(hipMalloc(&d_st, nw * 64));
+            cap = nw * 64;
+        }
+        HIPCHECK(hipMemset(d_st, 0, nw * 64));
+        P.stamps = d_st;
+        stamp_buf() = d_st;
+        stamp_n() = nw;
+    }
+#endif
     P.counters = s->d_counters;
 
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
     const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
     const bool use_lds = P.n_sph <= kLdsSphereCap;
-    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * (sizeof(double4) + sizeof(float4) + sizeof(float)) : 0;
-    HIPCHECK(hipMemsetAsync(s->d_counters, 0, 2 * sizeof(unsigned long long), st));
+    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * sizeof(double4) : 0;
+    HIPCHECK(hipMemsetAsync(s->d_counters, 0, 4 * sizeof(unsigned long long), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     if (P.n_rows) {
         const char *fenv = std::getenv("RTW_FILTER");  // 0 = brute-force f64 scan (A/B, tests)
@@ -621,12 +748,14 @@ void collect(rtw_session *s) {
     if (!s->pending) return;
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
-    unsigned long long c[2] = {0, 0};
+    unsigned long long c[4] = {0, 0, 0, 0};
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
     float ms = 0.f;
     HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last.segments = c[0];
     s->last.wave_iterations = c[1];
+    s->last.exact_tests = c[2];
+    s->last.exact_wave_iterations = c[3];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->pending = false;
@@ -648,7 +777,7 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&s->ev0));
         HIPCHECK(hipEventCreate(&s->ev1));
-        HIPCHECK(hipMalloc(&s->d_counters, 2 * sizeof(unsigned long long)));
+        HIPCHECK(hipMalloc(&s->d_counters, 4 * sizeof(unsigned long long)));
         upload_jump(s);
     } catch (...) {
         rtw_session_destroy(s);
@@ -693,9 +822,9 @@ int rtw_session_destroy(rtw_session *s) {
     if (!s) return RTW_OK;
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
-    dev_free(s->d_sph), dev_free(s->d_sph32), dev_free(s->d_sphw);
+    dev_free(s->d_sph), dev_free(s->d_filt);
     dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
-    dev_free(s->d_jump), dev_free(s->d_counters);
+    dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
@@ -798,6 +927,16 @@ int rtw_probe_device_seeds(int device, rtw_u128 seed, uint64_t first_pixel, uint
         return e.code;
     }
 }
+
+#ifdef RTW_STAMPS
+// Diagnostic: copies the per-wave stamp rows of the last render (8 u64 each).
+int rtw_diag_stamps(uint64_t *out, uint64_t cap_rows, uint64_t *n_rows) {
+    *n_rows = stamp_n();
+    if (!out || cap_rows < stamp_n()) return RTW_E_CAPACITY;
+    (void)hipDeviceSynchronize();
+    return hipMemcpy(out, stamp_buf(), stamp_n() * 64, hipMemcpyDeviceToHost) == hipSuccess ? RTW_OK : RTW_E_HIP;
+}
+#endif
 
 int rtw_probe_f64_ops(int device, const double *a, const double *b, uint64_t n, double *out_sqrt,
                       double *out_div) {

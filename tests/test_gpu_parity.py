@@ -229,3 +229,20 @@ def test_final_scene_config4_sampled_rows():
     fb, st = gpu(cam, sph, n, mt, nm, 23, SEED, shard=(300, 74, 2))
     ref, seg = oracle(cam, sph, n, mt, nm, 23, SEED, rows=(300, 74, 2))
     assert_same(fb, ref, st, seg)
+
+
+def test_deep_paths_use_spill_levels():
+    """Camera inside a closed Lambertian sphere: every path bounces to the depth
+    cap, so the path stack runs past its register slots into the HBM spill levels."""
+    world = rtw.SceneBuilder()
+    world.add(rtw.Sphere.new_world_obj(0., 0., 0., 10., rtw.Lambertian((0.93, 0.91, 0.97))))
+    world.add(rtw.Sphere.new_world_obj(0., -1., -3., 1., rtw.Metal((0.8, 0.85, 0.9), 0.2)))
+    world.add(rtw.Sphere.new_world_obj(1.5, 0., -3., 0.7, rtw.Dielectric(1.5)))
+    scene = world.build()
+    sph, n, mt, nm = scene.flatten()
+    for depth in (9, 40):
+        cam = rtw.Camera.new(24, 32, depth, 1.0, 80.0, (0., 0., 2.), (0., 0., -1.), (0., 1., 0.), 0.5, 5.0)
+        fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, 2, 31)
+        ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, 31)
+        assert_same(fb, ref, st, seg)
+        assert st.segments == st.samples * depth  # nothing ever escapes
