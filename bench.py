@@ -152,7 +152,7 @@ def main():
     out = None
     if rank == 0:
         out = {
-            "metric": "Msamples/sec (pixels x spp) on final-scene 1200x675 spp=500 d=50",
+            "metric": "Msamples/sec (pixels\u00d7spp) on final-scene 1200\u00d7675 spp=500 d=50; CPU-ref speedup",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
