@@ -13,17 +13,25 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
             -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
 
-all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check
 
-$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_accel.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/rtw_accel_build.o: $(SRC)/host/rtw_accel_build.cpp $(SRC)/rtw_accel.h
+	@mkdir -p $(OUT)
+	$(CXX) $(CXXFLAGS) -I$(SRC) -c $< -o $@
+
+# test infrastructure: host self-check of the BVH walk (tests/test_accel.py)
+$(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
+	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/accel_check.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
 
 $(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_host.o
+$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
 
 $(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
@@ -36,7 +44,7 @@ oracle:
 stamps: $(OUT)/librtw_stamps.so
 $(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
 	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
-$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_host.o
+$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
 asm: $(SRC)/rtw_render.hip

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -90,6 +90,10 @@ typedef struct rtw_stats {
     uint64_t exact_wave_iterations; /* wave-level iterations of the exact-test loop    */
     double kernel_ms;         /* render kernel time, HIP events on the launch stream   */
     uint32_t grid_blocks, block_threads;
+    uint64_t node_visits;     /* BVH walk iterations (inner-node or leaf tests), lanes  */
+    uint64_t brute_segments;  /* segments the BVH path re-did by brute-force scan      */
+    uint32_t accel;           /* 0 brute-force f64, 1 f32-filtered scan, 2 BVH         */
+    uint32_t lds_bytes;       /* dynamic LDS per workgroup                             */
 } rtw_stats;
 
 /* ---- library ---- */

@@ -69,7 +69,8 @@ class Stats(C.Structure):
                 ("sphere_tests", C.c_uint64), ("wave_iterations", C.c_uint64),
                 ("exact_tests", C.c_uint64), ("exact_wave_iterations", C.c_uint64),
                 ("kernel_ms", C.c_double), ("grid_blocks", C.c_uint32),
-                ("block_threads", C.c_uint32)]
+                ("block_threads", C.c_uint32), ("node_visits", C.c_uint64),
+                ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,0 +1,264 @@
+// rtw_accel.h -- exact-result sphere BVH for Scene::hit (hittable.rs:131-143).
+//
+// The reference tests every object and keeps the first minimum (`min_by` over
+// partial_cmp in insertion order). This header replaces the O(n) scan with a
+// conservative f32 BVH walk that provably returns the SAME (t, index) as the scan:
+//
+//   1. "always" spheres (huge radius, or outside the f32 guard) are tested exactly
+//      first, in index order;
+//   2. the BVH walk (f32) only collects candidate spheres; a node is skipped only
+//      if (a) the padded ray/box slab test proves the ray misses it, (b) its far
+//      end lies before t = 0.01 (Interval::from(0.01), camera.rs:387), or (c) its
+//      near end lies beyond U, a running estimate of the closest hit distance;
+//      a leaf is skipped only if the exact-conservative f32 discriminant filter
+//      proves the f64 discriminant negative (DESIGN.md "Exact pre-filter");
+//   3. candidates get the reference's own f64 Sphere::hit (sphere.rs:39-71) and
+//      the lexicographic (t, index) minimum -- the scan's first-minimum rule;
+//   4. verification: a cut by (c) is safe iff the final t <= U. U is only an
+//      estimate, so if the final hit is farther than U (or missing) the lane
+//      redoes the segment by brute force. Correctness rests on (a), (b), the leaf
+//      filter and this check, never on the quality of U.
+//
+// Padding (a): with o32 = fl32(o), e32 = fl32(d/|d|), the computed ray deviates
+// from the exact one by <= 5 u32 (|o|_max + M_b) at any point of a box whose
+// coordinates are bounded by M_b; f32 slab arithmetic adds ~3 u32 of the same
+// scale and the f64 root's tangent error is ~2^-26 |oc|. Every box is inflated by
+// kPadK * M_b on the host and every lane widens its slabs by kPadK * |o|_max, with
+// kPadK = 2^-16 (> 30x the bound).
+//
+// Shared by the device kernel (rtw_render.hip) and the host self-check
+// (tools/accel_check.cpp): one definition of the walk for both.
+#pragma once
+
+#include <cstdint>
+#include <cstring>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RTW_HD __host__ __device__ __forceinline__
+#else
+#define RTW_HD inline
+#endif
+#include <cmath>
+#include <vector>
+
+namespace rtw_accel {
+
+constexpr float kPadK = 1.52587890625e-05f;  // 2^-16
+constexpr double kPadKd = 1.52587890625e-05;
+constexpr float kDirFloor = 9.094947017729282e-13f;  // 2^-40: |e_i| clamp before 1/e_i
+constexpr float kGuardBvh = 1e8f;       // |origin| beyond -> brute force for the segment
+constexpr uint32_t kMaxSpheres = 2048;  // 12-bit node ids (2n - 1 <= 4095)
+constexpr uint32_t kMaxDepth = 12;      // register stack: 3 x u64 of 16-bit entries
+constexpr uint32_t kMaxAlways = 16;
+constexpr uint32_t kMaxCand = 8;        // candidate list: 2 x u64 of 16-bit entries
+constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -> "always"
+
+// Node (32 B, two float4): {lo.xyz, left | axis << 30}, {hi.xyz, right}.
+// Child id < n_inner -> inner node; else leaf (id - n_inner) in leaf order.
+// Leaf (32 B, two float4): {cx, cy, cz, R2'} (the pass-1 filter record) and
+// {d2, sphere index, 0, 0} with d2 >= 2 (R2' - r*r) (the filter's inflation, x2).
+
+RTW_HD uint32_t as_u32(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return u;
+}
+RTW_HD float as_f32(uint32_t u) {
+    float f;
+    memcpy(&f, &u, 4);
+    return f;
+}
+
+RTW_HD float rcp32(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+RTW_HD float fmin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+RTW_HD float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+
+// The reference's Sphere::hit (sphere.rs:39-71) in f64 with its operation order:
+// a = d.d (hoisted), hb = oc.d, c = oc.oc - r*r, disc = hb*hb - a*c; roots
+// (-sq - hb)/a then (sq - hb)/a, the first inside [0.01, inf] (interval.rs:55-57).
+RTW_HD bool sphere_hit_f64(double ox, double oy, double oz, double dx, double dy, double dz,
+                           double a, double cx, double cy, double cz, double rr, double &t) {
+    const double ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const double hb = ocx * dx + ocy * dy + ocz * dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rr;
+    const double disc = hb * hb - a * c;
+    if (disc < 0.) return false;
+    const double sq = __builtin_sqrt(disc);
+    t = (-sq - hb) / a;
+    if (!(t >= 0.01)) t = (sq - hb) / a;
+    return t >= 0.01;
+}
+
+// Exact-conservative f32 pre-filter of the discriminant (DESIGN.md "Exact
+// pre-filter"): records carry R2' >= r*r + K (m_c^2 + r*r/2) (host, rounded up)
+// and a lane with origin magnitude m_o keeps a sphere unless disc32 < -G,
+// G = K m_o^2 + floor. K = 2^-15 = 512 u32 (the first-order bound needs 163 u32).
+constexpr double kFilterK = 3.0517578125e-05;  // 2^-15
+constexpr double kFilterFloor = 1e-25;         // f32 underflow errors inside the guard
+constexpr double kGuardHi = 1e12;              // max |origin| / |center| component for f32
+
+RTW_HD float filter_neg_g(double mo) {
+    return -static_cast<float>(fma(kFilterK * mo, mo * 1.000001, kFilterFloor));
+}
+
+// Per-segment ray state for the f32 walk.
+struct WalkRay {
+    float ox, oy, oz;   // o32
+    float ex, ey, ez;   // e32 (filter direction, ~unit)
+    float ix, iy, iz;   // 1 / clamped e32
+    float alx, aly, alz, ahx, ahy, ahz;  // -(o -/+ pad) * inv: slab offsets, padded outward
+    float tmin;         // 0.01 |d| rounded down (distance units)
+    float negG;         // -(filter margin G)
+    uint32_t neg;       // bit k: e32 component k < 0 (near child = right on that axis)
+};
+
+RTW_HD float clamp_dir(float e) {
+    return fabsf(e) < kDirFloor ? (e < 0.f ? -kDirFloor : kDirFloor) : e;
+}
+
+// o32/e32 as used by the pass-1 filter (e32 = fl32(d / sqrt(a))), mo = max |o_i|
+// (f64), sa = sqrt(a). Returns false if the segment must be brute-forced
+// (non-finite or out-of-guard ray).
+RTW_HD bool walk_setup(float ox, float oy, float oz, float ex, float ey, float ez, double mo,
+                       double sa, float negG, WalkRay &r) {
+    if (!(mo <= static_cast<double>(kGuardBvh)) || !(sa > 0.) || !(sa < 1e30)) return false;
+    if (!(fabsf(ex) <= 2.f) || !(fabsf(ey) <= 2.f) || !(fabsf(ez) <= 2.f)) return false;
+    r.ox = ox, r.oy = oy, r.oz = oz, r.ex = ex, r.ey = ey, r.ez = ez;
+    r.neg = (ex < 0.f ? 1u : 0u) | (ey < 0.f ? 2u : 0u) | (ez < 0.f ? 4u : 0u);
+    r.ix = rcp32(clamp_dir(ex)), r.iy = rcp32(clamp_dir(ey)), r.iz = rcp32(clamp_dir(ez));
+    const float pad = kPadK * static_cast<float>(mo) + 1e-30f;
+    r.alx = -(ox + pad) * r.ix, r.ahx = -(ox - pad) * r.ix;
+    r.aly = -(oy + pad) * r.iy, r.ahy = -(oy - pad) * r.iy;
+    r.alz = -(oz + pad) * r.iz, r.ahz = -(oz - pad) * r.iz;
+    r.tmin = static_cast<float>(0.01 * sa * (1. - 1e-6));
+    r.negG = negG;
+    return true;
+}
+
+// U seeded from an exact hit at parameter t: the distance t*sa, rounded up with
+// room for the final check below.
+RTW_HD float seed_cut(double t, double sa) {
+    return static_cast<float>(t * sa * (1. + 1. / 262144.)) * (1.f + 2.4e-7f);
+}
+// The cut was safe iff the final hit is no farther than U (module comment, 4).
+RTW_HD bool cut_ok(float U, int best, double bt, double sa) {
+    return !(U < INFINITY) || (best >= 0 && bt * sa <= static_cast<double>(U) * (1. - 1. / 1048576.));
+}
+
+RTW_HD float sqrt32(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sqrtf(x);  // U is an estimate: the approximate root suffices
+#else
+    return sqrtf(x);
+#endif
+}
+
+// Collects the leaves (leaf-order ids) the walk cannot rule out. U (distance
+// units along e32) is the running cut; the caller seeds it from the "always"
+// spheres. Returns false on candidate-list overflow (caller brute-forces).
+// `visits` counts loop iterations (node or leaf tests).
+template <typename F4>
+RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, uint32_t n_inner,
+                 const WalkRay &r, float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc,
+                 uint32_t &visits) {
+    uint64_t s0 = 0, s1 = 0, s2 = 0;
+    uint32_t sp = 0, cur = 0;
+    bool ok = true;
+    for (;;) {
+        ++visits;
+        if (cur < n_inner) {
+            const F4 A = nodes[2 * cur], B = nodes[2 * cur + 1];
+            const float t0x = fmaf(A.x, r.ix, r.alx), t1x = fmaf(B.x, r.ix, r.ahx);
+            const float t0y = fmaf(A.y, r.iy, r.aly), t1y = fmaf(B.y, r.iy, r.ahy);
+            const float t0z = fmaf(A.z, r.iz, r.alz), t1z = fmaf(B.z, r.iz, r.ahz);
+            const float nr = fmax3(fminf(t0x, t1x), fminf(t0y, t1y), fminf(t0z, t1z));
+            const float fr = fmin3(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fmaxf(t0z, t1z));
+            if (!(nr > fr) && !(fr < r.tmin) && !(nr > U)) {
+                const uint32_t L = as_u32(A.w), R = as_u32(B.w);
+                const uint32_t lid = L & 0xffffu;
+                const bool right_first = (r.neg >> (L >> 30)) & 1u;
+                const uint32_t near_c = right_first ? R : lid, far_c = right_first ? lid : R;
+                s2 = (s2 << 16) | (s1 >> 48);
+                s1 = (s1 << 16) | (s0 >> 48);
+                s0 = (s0 << 16) | far_c;
+                ++sp;
+                cur = near_c;
+                continue;
+            }
+        } else {
+            const uint32_t k = cur - n_inner;
+            const F4 S = leaves[2 * k];
+            const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
+            const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
+            const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+            const float disc = fmaf(hb, hb, -cc);
+            if (!(disc < r.negG)) {
+                if (nc < kMaxCand) {
+                    if (nc < 4) c0 |= static_cast<uint64_t>(k) << (16u * nc);
+                    else c1 |= static_cast<uint64_t>(k) << (16u * (nc - 4u));
+                    ++nc;
+                } else {
+                    ok = false;
+                }
+                // A sure hit (disc beyond the filter's inflation + error, far root
+                // clearly past tmin) bounds the closest hit by its far root.
+                const float d2 = leaves[2 * k + 1].x;
+                if (disc > d2 - 2.f * r.negG) {
+                    const float sd = sqrt32(disc);
+                    const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
+                    const float sfar = sd - hb;
+                    const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
+                    if (slo - slack > r.tmin * 1.001f) U = fminf(U, sfar + slack);
+                }
+            }
+        }
+        if (sp == 0) break;
+        cur = static_cast<uint32_t>(s0 & 0xffffu);
+        s0 = (s0 >> 16) | (s1 << 48);
+        s1 = (s1 >> 16) | (s2 << 48);
+        s2 >>= 16;
+        --sp;
+    }
+    return ok;
+}
+
+RTW_HD uint32_t cand_at(uint64_t c0, uint64_t c1, uint32_t j) {
+    return static_cast<uint32_t>((j < 4 ? c0 >> (16u * j) : c1 >> (16u * (j - 4u))) & 0xffffu);
+}
+
+// (t, i) beats (bt, best) under the scan's first-minimum rule.
+RTW_HD bool better(double t, uint32_t i, double bt, int best) {
+    return best < 0 || t < bt || (t == bt && static_cast<int>(i) < best);
+}
+
+// ---- host only (declared in both compilation passes, defined for the host) ----
+// R2' of the pass-1 record of a sphere (center c, r*r = rr); +inf (always tested
+// exactly) outside the guard or for non-finite input.
+inline float filter_r2p(const double *c, double rr) {
+    const double mc = std::fmax(std::fmax(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2]));
+    if (!(mc <= kGuardHi) || !std::isfinite(rr)) return INFINITY;
+    const double x = rr + kFilterK * (mc * mc + rr / 2.) * (1. + 1e-6);
+    if (!(x >= 0.) || !(x <= 1e36)) return INFINITY;
+    return std::nextafter(static_cast<float>(x), INFINITY);
+}
+
+// Host builder (rtw_accel_build.cpp). Spheres as centers (3n f64) and radii;
+// r2p = the pass-1 filter's R2' per sphere (the same records the brute-force
+// filter uses). Returns false if the scene is not eligible (n > kMaxSpheres or
+// too many "always" spheres): the kernel then scans by brute force.
+struct Bvh {
+    uint32_t n_inner = 0, n_leaf = 0, depth = 0;
+    std::vector<float> nodes;      // 8 floats per inner node (two float4)
+    std::vector<float> leaves;     // 8 floats per leaf (two float4)
+    std::vector<uint32_t> always;  // sphere indices tested exactly first, ascending
+};
+bool build(const double *centers, const double *radii, const float *r2p, uint32_t n, Bvh &out);
+
+}  // namespace rtw_accel

@@ -31,6 +31,7 @@
 #include <string>
 #include <vector>
 
+#include "rtw_accel.h"
 #include "rtw_capi.h"
 #include "host/rtw_host.h"
 #include "host/rtw_internal.h"
@@ -39,16 +40,18 @@ namespace {
 
 constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 constexpr int kTile = 16;
-constexpr uint32_t kLdsSphereCap = 2048;  // exact f64 records staged in LDS: <= 64 KiB
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
+constexpr size_t kLdsCap = 64 * 1024;     // dynamic LDS per workgroup
+constexpr int kCounters = 6;
 
-// Exact-conservative f32 pre-filter of Sphere::hit's discriminant (derivation in
-// the pass-1 comment and DESIGN.md "Exact pre-filter"). K = 2^-15 = 512 u32; the
-// first-order error bound needs 163 u32.
-constexpr double kFilterK = 3.0517578125e-05;   // 2^-15
-constexpr double kFilterFloor = 1e-25;          // f32 underflow errors inside the guard
-constexpr double kGuardHi = 1e12;               // max |origin| component for the f32 pass
+// Scene::hit strategies (one kernel instantiation each)
+constexpr int kScanF64 = 0;  // the reference's scan, f64 only
+constexpr int kScanF32 = 1;  // scan behind the exact-conservative f32 filter
+constexpr int kBvh = 2;      // rtw_accel.h walk + exact candidates (+ scan fallback)
+
+using rtw_accel::kFilterK;
+using rtw_accel::kGuardHi;
 
 // Wave-uniform load of a pass-1 record through the constant address space, so the
 // compiler emits s_load (4 records per s_load_dwordx16) and feeds SGPR operands.
@@ -57,6 +60,14 @@ __device__ __forceinline__ float4 ld_filt(const float4 *p, uint32_t i) {
     typedef const __attribute__((address_space(4))) float cfloat;
     const cfloat *q = (const cfloat *)(p);
     return make_float4(q[4 * i], q[4 * i + 1], q[4 * i + 2], q[4 * i + 3]);
+#else
+    return p[i];
+#endif
+}
+__device__ __forceinline__ uint32_t ld_const_u32(const uint32_t *p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    return ((const cu32 *)(p))[i];
 #else
     return p[i];
 #endif
@@ -73,9 +84,13 @@ struct KParams {
     uint32_t W, s, n_off, max_depth;
     uint32_t row_begin, row_step, n_rows, n_sph;
     uint32_t jump_bits, _pad;
+    uint32_t n_inner, n_leaf, n_always, _pad2;
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
+    const float4 *nodes;        // BVH inner nodes, 2 float4 each (rtw_accel.h)
+    const float4 *leaves;       // BVH leaves, 2 float4 each
+    const uint32_t *always;     // spheres tested exactly before the walk
     const double *radius;       // r
     const uint32_t *sph_mat;    // material row per sphere
     const rtw_material *mats;   // material table
@@ -83,7 +98,8 @@ struct KParams {
     double *out;                // n_rows * W * 3
     uint16_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
-    unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests, [3] wave exact-pass iterations
+    unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
+                                   // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -214,22 +230,32 @@ __device__ __forceinline__ uint64_t stamp_now() {
 #endif
 
 // ---------------------------------------------------------------- megakernel --
-template <bool kLds, bool kFilter>
+template <bool kLds, int kMode>
 __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
-    // LDS: exact f64 sphere records for the per-lane candidate pass.
+    // LDS: exact f64 sphere records, then (BVH mode) the inner nodes and leaves.
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const uint32_t n = P.n_sph;
     const double4 *__restrict__ sph = P.sph;
+    const float4 *__restrict__ nodes = P.nodes;
+    const float4 *__restrict__ leaves = P.leaves;
     if (kLds) {
         for (uint32_t i = threadIdx.x; i < n; i += kBlock) lds_sph[i] = P.sph[i];
+        float4 *lf = reinterpret_cast<float4 *>(lds_sph + n);
+        if (kMode == kBvh) {
+            const uint32_t nn = 2u * P.n_inner, nl = 2u * P.n_leaf;
+            for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lf[i] = P.nodes[i];
+            for (uint32_t i = threadIdx.x; i < nl; i += kBlock) lf[nn + i] = P.leaves[i];
+        }
         __syncthreads();
         sph = lds_sph;
+        nodes = lf;
+        leaves = lf + 2u * P.n_inner;
     }
     const float4 *filt = P.filt;
 
     const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
     const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
-    uint32_t seg = 0, ntest = 0, nwave2 = 0;
+    uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0;
     const uint32_t lane = threadIdx.x & 63u;
     STAMP_DECL
 
@@ -285,13 +311,14 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
             gen_ray(0);
             STAMP(0);  // 0: seed jump + pixel setup
             for (;;) {
-                // ---- Scene::hit: all spheres, first minimum wins ----
+                // ---- Scene::hit (hittable.rs:131-143): first minimum over all spheres ----
                 ++seg;
                 const double a = dx * dx + dy * dy + dz * dz;
                 int best = -1;
                 double bt = 0.;
 
-                // ---- pass 1 setup: f32 unit direction e, per-lane margin G ----
+                // ---- f32 setup shared by the filter and the walk: unit direction e,
+                // per-lane margin G ----
                 // Exact-conservative filter. With ê = d/|d| the discriminant's sign is
                 // that of D' = (OC.ê)^2 - (|OC|^2 - R2) = D / a. Computed in f32 with
                 // oc = o32 - c32, e = fl32(ê), and R2' >= R2 + K (m_c^2 + R2/2) in
@@ -302,64 +329,101 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                 // so every sphere whose f64 discriminant is >= 0 (or NaN) passes the
                 // test disc32 >= -G, G = K m_o^2 + floor. NaN/inf anywhere -> kept.
                 const double mo64 = fmax(fmax(__builtin_fabs(ox), __builtin_fabs(oy)), __builtin_fabs(oz));
-                const bool fast = kFilter && mo64 <= kGuardHi;  // false for NaN too
-                const double inv = 1.0 / __builtin_sqrt(a);
+                const bool fast = kMode != kScanF64 && mo64 <= kGuardHi;  // false for NaN too
+                const double sa = __builtin_sqrt(a);
+                const double inv = 1.0 / sa;
                 const float ex = static_cast<float>(dx * inv), ey = static_cast<float>(dy * inv),
                             ez = static_cast<float>(dz * inv);
                 const float o32x = static_cast<float>(ox), o32y = static_cast<float>(oy),
                             o32z = static_cast<float>(oz);
-                const float negG = -static_cast<float>(fma(kFilterK * mo64, mo64 * 1.000001, kFilterFloor));
+                const float negG = rtw_accel::filter_neg_g(mo64);
 
-                STAMP(5);  // 5: segment setup
-                for (uint32_t base = 0; base < n; base += kChunk) {
-                    const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
-                    // sphere base+j is bit (31 - j): highest set bit = lowest index
-                    uint32_t mask;
-                    if (fast) {
-                        mask = 0;
-                        for (uint32_t g = 0; g < static_cast<uint32_t>(kChunk); g += kGroup) {
+                // exact f64 Sphere::hit (sphere.rs:39-71) of sphere i; keeps the
+                // lexicographic (t, index) minimum = the scan's first-minimum rule
+                auto exact = [&](uint32_t i) {
+                    ++ntest;
+                    const double4 S = sph[i];
+                    double t;
+                    if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t) &&
+                        rtw_accel::better(t, i, bt, best)) {
+                        bt = t;
+                        best = static_cast<int>(i);
+                    }
+                };
+                // f32 filter value for one pass-1 record (wave-uniform SGPR operand)
+                auto filt_pass = [&](const float4 S) {
+                    const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
+                    const float hb = fmaf(ocx, ex, fmaf(ocy, ey, ocz * ez));
+                    const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+                    const float disc = fmaf(hb, hb, -cc);
+                    return !(disc < negG);
+                };
+                // The scan: every sphere in index order, pass 1 (f32 filter, wave-
+                // uniform) then pass 2 (f64, per lane, the lane's candidates only).
+                auto scan = [&](bool use_filter) {
+                    best = -1;
+                    for (uint32_t base = 0; base < n; base += kChunk) {
+                        const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
+                        // sphere base+j is bit (31 - j): highest set bit = lowest index
+                        uint32_t mask;
+                        if (use_filter) {
+                            mask = 0;
+                            for (uint32_t g = 0; g < static_cast<uint32_t>(kChunk); g += kGroup) {
 #pragma unroll
-                            for (int j = 0; j < kGroup; ++j) {
-                                const float4 S = ld_filt(filt, base + g + j);  // wave-uniform: s_load
-                                const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
-                                const float hb = fmaf(ocx, ex, fmaf(ocy, ey, ocz * ez));
-                                const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-                                const float disc = fmaf(hb, hb, -cc);
-                                mask = mask + mask + static_cast<uint32_t>(!(disc < negG));
+                                for (int j = 0; j < kGroup; ++j)
+                                    mask = mask + mask + static_cast<uint32_t>(filt_pass(ld_filt(filt, base + g + j)));
+                            }
+                            if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
+                        } else {
+                            mask = cnt == static_cast<uint32_t>(kChunk) ? ~0u : ~((1u << (kChunk - cnt)) - 1u);
+                        }
+                        STAMP(1);  // 1: pass 1 (f32 filter)
+                        while (mask) {
+                            {  // the wave's first active lane counts the wave-level iteration
+                                const uint64_t exm = __builtin_amdgcn_read_exec();
+                                nwave2 += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
+                            }
+                            const uint32_t top = 31u - static_cast<uint32_t>(__builtin_clz(mask));
+                            mask ^= 1u << top;
+                            exact(base + (31u - top));
+                        }
+                        STAMP(2);  // 2: pass 2 (exact f64 tests)
+                    }
+                };
+
+                if constexpr (kMode == kBvh) {
+                    bool brute = !fast;
+                    if (fast) {
+                        for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
+                            const uint32_t i = ld_const_u32(P.always, j);
+                            if (filt_pass(ld_filt(filt, i))) exact(i);
+                        }
+                        rtw_accel::WalkRay wr;
+                        if (P.n_leaf == 0) {
+                        } else if (!rtw_accel::walk_setup(o32x, o32y, o32z, ex, ey, ez, mo64, sa, negG, wr)) {
+                            brute = true;
+                        } else {
+                            float U = best >= 0 ? rtw_accel::seed_cut(bt, sa) : INFINITY;
+                            uint64_t c0 = 0, c1 = 0;
+                            uint32_t nc = 0;
+                            if (!rtw_accel::walk(nodes, leaves, P.n_inner, wr, U, c0, c1, nc, visits)) {
+                                brute = true;
+                            } else {
+                                for (uint32_t j = 0; j < nc; ++j) {
+                                    const uint32_t leaf = rtw_accel::cand_at(c0, c1, j);
+                                    exact(__float_as_uint(leaves[2u * leaf + 1u].y));
+                                }
+                                brute = !rtw_accel::cut_ok(U, best, bt, sa);
                             }
                         }
-                        if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
-                    } else {
-                        mask = cnt == static_cast<uint32_t>(kChunk) ? ~0u : ~((1u << (kChunk - cnt)) - 1u);
                     }
-                    STAMP(1);  // 1: pass 1 (f32 filter)
-                    // Pass 2 (f64, exactly sphere.rs:39-71) on this lane's
-                    // candidates, in index order.
-                    while (mask) {
-                        ++ntest;
-                        {  // the wave's first active lane counts the wave-level iteration
-                            const uint64_t exm = __builtin_amdgcn_read_exec();
-                            nwave2 += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
-                        }
-                        const uint32_t top = 31u - static_cast<uint32_t>(__builtin_clz(mask));
-                        mask ^= 1u << top;
-                        const uint32_t i = base + (31u - top);
-                        const double4 S = sph[i];
-                        const double ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
-                        const double hb = ocx * dx + ocy * dy + ocz * dz;
-                        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - S.w;
-                        const double disc = hb * hb - a * c;
-                        if (!(disc < 0.)) {
-                            const double sq = __builtin_sqrt(disc);
-                            double t = (-sq - hb) / a;
-                            if (!(t >= 0.01)) t = (sq - hb) / a;
-                            if (t >= 0.01 && (best < 0 || t < bt)) {
-                                bt = t;
-                                best = static_cast<int>(i);
-                            }
-                        }
+                    if (brute) {
+                        ++nbrute;
+                        scan(fast);
                     }
-                    STAMP(2);  // 2: pass 2 (exact f64 tests)
+                    STAMP(1);
+                } else {
+                    scan(fast);
                 }
 
                 bool finish;
@@ -485,6 +549,8 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&P.counters[1], static_cast<unsigned long long>(m));
         if (ntest) atomicAdd(&P.counters[2], static_cast<unsigned long long>(ntest));
         if (nwave2) atomicAdd(&P.counters[3], static_cast<unsigned long long>(nwave2));
+        if (visits) atomicAdd(&P.counters[4], static_cast<unsigned long long>(visits));
+        if (nbrute) atomicAdd(&P.counters[5], static_cast<unsigned long long>(nbrute));
     }
 }
 
@@ -532,6 +598,11 @@ struct rtw_session {
     size_t spill_bytes = 0;
     uint32_t n_sph = 0, n_mats = 0;
     bool scene_set = false;
+    // BVH (rtw_accel.h); has_bvh = false -> the filtered scan
+    float4 *d_nodes = nullptr, *d_leaves = nullptr;
+    uint32_t *d_always = nullptr;
+    uint32_t n_inner = 0, n_leaf = 0, n_always = 0;
+    bool has_bvh = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t last_stream = nullptr;
     bool pending = false;
@@ -568,19 +639,17 @@ void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uin
         if (sp[i].mat >= nm) throw rtw::Error(RTW_E_MAT_INDEX, "sphere material index out of range");
 }
 
-// f32 value >= x (x finite, >= 0): round to nearest, then one ulp up.
-float round_up_f32(double x) {
-    if (!(x >= 0.) || !(x <= 1e36)) return INFINITY;
-    return std::nextafter(static_cast<float>(x), INFINITY);
-}
-
 void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
     dev_free(s->d_sph), dev_free(s->d_filt);
     dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     s->d_sph = nullptr, s->d_filt = nullptr;
     s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
+    s->d_nodes = nullptr, s->d_leaves = nullptr, s->d_always = nullptr;
+    s->has_bvh = false, s->scene_set = false;
+    s->n_inner = s->n_leaf = s->n_always = 0;
     const uint32_t npad = (n + kChunk - 1) / kChunk * kChunk;
     std::vector<double4> a(n ? n : 1);
     // padding records can never be candidates (R2' = -inf -> disc = -inf)
@@ -594,10 +663,7 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         a[i] = make_double4(c[0], c[1], c[2], rr);
         // R2' >= r*r + K (m_c^2 + r*r/2), m_c = max |c_i|, rounded up to f32; +inf
         // (always tested exactly) outside the guard or for non-finite input.
-        const double mc = std::fmax(std::fmax(std::fabs(c[0]), std::fabs(c[1])), std::fabs(c[2]));
-        const float r2p = (mc <= kGuardHi && std::isfinite(rr))
-                              ? round_up_f32(rr + kFilterK * (mc * mc + rr / 2.) * (1. + 1e-6))
-                              : INFINITY;
+        const float r2p = rtw_accel::filter_r2p(c, rr);
         f[i] = make_float4(static_cast<float>(c[0]), static_cast<float>(c[1]),
                            static_cast<float>(c[2]), r2p);
         r[i] = rad;
@@ -613,6 +679,31 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
     HIPCHECK(hipMemcpy(s->d_rad, r.data(), r.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_smat, mi.data(), mi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     if (nm) HIPCHECK(hipMemcpy(s->d_mats, m, nm * sizeof(rtw_material), hipMemcpyHostToDevice));
+    // BVH over the same records (rtw_accel_build.cpp); ineligible scenes scan
+    {
+        std::vector<double> cen(3 * static_cast<size_t>(n)), rad(n);
+        std::vector<float> r2p(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            for (int k = 0; k < 3; ++k) cen[3 * i + k] = sp[i].center[k];
+            rad[i] = sp[i].radius;
+            r2p[i] = f[i].w;
+        }
+        rtw_accel::Bvh bvh;
+        if (n && rtw_accel::build(cen.data(), rad.data(), r2p.data(), n, bvh)) {
+            const size_t nb = bvh.nodes.size() * sizeof(float), lb = bvh.leaves.size() * sizeof(float);
+            HIPCHECK(hipMalloc(&s->d_nodes, nb ? nb : 16));
+            HIPCHECK(hipMalloc(&s->d_leaves, lb ? lb : 16));
+            HIPCHECK(hipMalloc(&s->d_always, (bvh.always.size() + 1) * sizeof(uint32_t)));
+            if (nb) HIPCHECK(hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice));
+            if (lb) HIPCHECK(hipMemcpy(s->d_leaves, bvh.leaves.data(), lb, hipMemcpyHostToDevice));
+            if (!bvh.always.empty())
+                HIPCHECK(hipMemcpy(s->d_always, bvh.always.data(), bvh.always.size() * sizeof(uint32_t),
+                                   hipMemcpyHostToDevice));
+            s->n_inner = bvh.n_inner, s->n_leaf = bvh.n_leaf;
+            s->n_always = static_cast<uint32_t>(bvh.always.size());
+            s->has_bvh = true;
+        }
+    }
     s->n_sph = n;
     s->n_mats = nm;
     s->scene_set = true;
@@ -676,6 +767,12 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.row_step = sh.row_step;
     P.n_rows = sh.n_rows;
     P.n_sph = s->n_sph;
+    P.n_inner = s->n_inner;
+    P.n_leaf = s->n_leaf;
+    P.n_always = s->n_always;
+    P.nodes = s->d_nodes;
+    P.leaves = s->d_leaves;
+    P.always = s->d_always;
     P.jump_bits = bits;
     P.seed_lo = seed.lo;
     P.seed_hi = seed.hi;
@@ -721,17 +818,30 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
     const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
-    const bool use_lds = P.n_sph <= kLdsSphereCap;
-    const size_t lds = use_lds ? static_cast<size_t>(P.n_sph) * sizeof(double4) : 0;
-    HIPCHECK(hipMemsetAsync(s->d_counters, 0, 4 * sizeof(unsigned long long), st));
+    // Scene::hit strategy: RTW_ACCEL=0 f64 scan, 1 filtered scan, 2 BVH (default
+    // when the scene is eligible); A/B and tests only -- results are identical.
+    int mode = s->has_bvh ? kBvh : kScanF32;
+    if (const char *e = std::getenv("RTW_ACCEL")) mode = std::atoi(e);
+    if (mode == kBvh && !s->has_bvh) mode = kScanF32;
+    if (mode < kScanF64 || mode > kBvh) mode = kScanF32;
+    size_t lds = static_cast<size_t>(P.n_sph) * sizeof(double4);
+    if (mode == kBvh) lds += (static_cast<size_t>(P.n_inner) + P.n_leaf) * 2 * sizeof(float4);
+    const bool use_lds = lds <= kLdsCap;
+    if (!use_lds) lds = 0;
+    HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     if (P.n_rows) {
-        const char *fenv = std::getenv("RTW_FILTER");  // 0 = brute-force f64 scan (A/B, tests)
-        const bool filt = fenv ? std::atoi(fenv) != 0 : true;
-        if (use_lds && filt) hipLaunchKernelGGL((rtw_render_f64<true, true>), grid, dim3(kBlock), lds, st, P);
-        else if (use_lds) hipLaunchKernelGGL((rtw_render_f64<true, false>), grid, dim3(kBlock), lds, st, P);
-        else if (filt) hipLaunchKernelGGL((rtw_render_f64<false, true>), grid, dim3(kBlock), 0, st, P);
-        else hipLaunchKernelGGL((rtw_render_f64<false, false>), grid, dim3(kBlock), 0, st, P);
+#define RTW_LAUNCH(L, M) hipLaunchKernelGGL((rtw_render_f64<L, M>), grid, dim3(kBlock), lds, st, P)
+        if (use_lds) {
+            if (mode == kBvh) RTW_LAUNCH(true, kBvh);
+            else if (mode == kScanF32) RTW_LAUNCH(true, kScanF32);
+            else RTW_LAUNCH(true, kScanF64);
+        } else {
+            if (mode == kBvh) RTW_LAUNCH(false, kBvh);
+            else if (mode == kScanF32) RTW_LAUNCH(false, kScanF32);
+            else RTW_LAUNCH(false, kScanF64);
+        }
+#undef RTW_LAUNCH
         HIPCHECK(hipGetLastError());
     }
     HIPCHECK(hipEventRecord(s->ev1, st));
@@ -742,13 +852,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     s->last.samples = s->last.pixels * P.n_off;
     s->last.grid_blocks = grid.x * grid.y;
     s->last.block_threads = kBlock;
+    s->last.accel = static_cast<uint32_t>(mode);
+    s->last.lds_bytes = static_cast<uint32_t>(lds);
 }
 
 void collect(rtw_session *s) {
     if (!s->pending) return;
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
-    unsigned long long c[4] = {0, 0, 0, 0};
+    unsigned long long c[kCounters] = {};
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
     float ms = 0.f;
     HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -756,6 +868,8 @@ void collect(rtw_session *s) {
     s->last.wave_iterations = c[1];
     s->last.exact_tests = c[2];
     s->last.exact_wave_iterations = c[3];
+    s->last.node_visits = c[4];
+    s->last.brute_segments = c[5];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->pending = false;
@@ -777,7 +891,7 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&s->ev0));
         HIPCHECK(hipEventCreate(&s->ev1));
-        HIPCHECK(hipMalloc(&s->d_counters, 4 * sizeof(unsigned long long)));
+        HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         upload_jump(s);
     } catch (...) {
         rtw_session_destroy(s);
@@ -825,6 +939,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_sph), dev_free(s->d_filt);
     dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
+    dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
