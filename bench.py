@@ -193,6 +193,7 @@ def main():
             "stats": {"accel": ["scan_f64", "scan_f32_filter", "bvh"][st.accel],
                       "node_visits_per_segment": round(st.node_visits / max(1, st.segments), 3),
                       "brute_segments": st.brute_segments, "lds_bytes": st.lds_bytes,
+                      "parked_pixels": st.parked_pixels,
                       "segments": st.segments, "segments_per_sample": round(st.segments / max(1, st.samples), 4),
                       "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),

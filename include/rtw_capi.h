@@ -94,6 +94,7 @@ typedef struct rtw_stats {
     uint64_t brute_segments;  /* segments the BVH path re-did by brute-force scan      */
     uint32_t accel;           /* 0 brute-force f64, 1 f32-filtered scan, 2 BVH         */
     uint32_t lds_bytes;       /* dynamic LDS per workgroup                             */
+    uint64_t parked_pixels;   /* pixels finished by the cooperative second kernel      */
 } rtw_stats;
 
 /* ---- library ---- */
@@ -170,6 +171,12 @@ int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_s
                        void *hip_stream);
 /* Waits for the session's last render and reports its statistics. */
 int rtw_session_stats(rtw_session *s, rtw_stats *out);
+/* Diagnostic (not part of the reference surface): per-pixel records of the last
+ * render when it ran with RTW_DIAG=1 in the environment -- for pixel p of the
+ * shard (row-major), out[2p] = traced segments of the pixel in the one-lane
+ * kernel, out[2p+1] = low 32 bits of the 100 MHz device real-time clock when
+ * the pixel completed or parked there (0 = never ran). Returns RTW_E_CAPACITY if cap < 2 x pixels. */
+int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap);
 
 /* ---- device probes (tests) ---- */
 /* Device jump-ahead seeds (the kernel's own code path) for a pixel range. */

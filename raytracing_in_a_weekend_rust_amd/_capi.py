@@ -70,7 +70,8 @@ class Stats(C.Structure):
                 ("exact_tests", C.c_uint64), ("exact_wave_iterations", C.c_uint64),
                 ("kernel_ms", C.c_double), ("grid_blocks", C.c_uint32),
                 ("block_threads", C.c_uint32), ("node_visits", C.c_uint64),
-                ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32)]
+                ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32),
+                ("parked_pixels", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -112,6 +113,7 @@ SIGNATURES = {
     "rtw_session_render": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, _P(Shard),
                                      C.c_void_p, C.c_void_p]),
     "rtw_session_stats": (C.c_int, [C.c_void_p, _P(Stats)]),
+    "rtw_session_diag": (C.c_int, [C.c_void_p, _P(C.c_uint32), C.c_uint64]),
     "rtw_probe_device_seeds": (C.c_int, [C.c_int, U128, C.c_uint64, C.c_uint64, _P(U128)]),
     "rtw_probe_f64_ops": (C.c_int, [C.c_int, _P(C.c_double), _P(C.c_double), C.c_uint64,
                                     _P(C.c_double), _P(C.c_double)]),

@@ -260,6 +260,13 @@ class Session:
         check(lib.rtw_session_stats(self.h, C.byref(st)))
         return st
 
+    def diag(self, n_pixels: int):
+        """RTW_DIAG=1 renders: per-pixel (segments, clock/1024 at completion)."""
+        import numpy as np
+        out = np.zeros(2 * n_pixels, dtype=np.uint32)
+        check(lib.rtw_session_diag(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        return out.reshape(n_pixels, 2)
+
     def close(self):
         if self.h:
             lib.rtw_session_destroy(self.h)

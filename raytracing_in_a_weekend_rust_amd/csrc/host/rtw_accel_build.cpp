@@ -4,10 +4,11 @@
 // skip spheres it can prove irrelevant, and the kernel still returns the scan's
 // (t, first index) result.
 //
-// Object-median split on the longest centroid axis, one sphere per leaf, so the
-// depth is ceil(log2 n) (<= 11 for n <= 2048): the kernel's register stack holds
-// 12 entries. Inner nodes are numbered in pre-order (root 0), leaves in walk
-// order; a child id >= n_inner names leaf (id - n_inner).
+// 4-wide nodes built top-down: a set of more than 4 spheres is cut into 4 parts
+// by two levels of object-median splits on the longest centroid axis; each node
+// holds the padded boxes of its (up to) 4 children -- inner nodes or single
+// spheres -- and per ray-octant near-to-far child orders. Boxes are inflated by kPadK * M_b and rounded outward
+// to f32 (rtw_accel.h "Padding").
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -35,9 +36,9 @@ struct Builder {
     const float *r2p;
     std::vector<uint32_t> idx;
     Bvh *out;
-    uint32_t next_inner = 0, next_leaf = 0, n_inner = 0, max_depth = 0;
+    uint32_t n_leaf = 0;
 
-    void box_of(uint32_t b, uint32_t e, double lo[3], double hi[3]) const {
+    void bounds(uint32_t b, uint32_t e, double lo[3], double hi[3]) const {
         for (int k = 0; k < 3; ++k) lo[k] = INFINITY, hi[k] = -INFINITY;
         for (uint32_t j = b; j < e; ++j) {
             const uint32_t i = idx[j];
@@ -49,23 +50,8 @@ struct Builder {
         }
     }
 
-    // Builds idx[b, e); returns the child id of the subtree's root.
-    uint32_t node(uint32_t b, uint32_t e, uint32_t depth) {
-        if (e - b == 1) {
-            const uint32_t k = next_leaf++, i = idx[b];
-            float *L = &out->leaves[8 * static_cast<size_t>(k)];
-            L[0] = static_cast<float>(c[3 * i]), L[1] = static_cast<float>(c[3 * i + 1]);
-            L[2] = static_cast<float>(c[3 * i + 2]), L[3] = r2p[i];
-            const double rr = r[i] * r[i];
-            L[4] = up_f32((2. * (static_cast<double>(r2p[i]) - rr)) * (1. + 1e-6));
-            L[5] = as_f32(i), L[6] = 0.f, L[7] = 0.f;
-            return n_inner + k;
-        }
-        max_depth = std::max(max_depth, depth);
-        const uint32_t id = next_inner++;
-        double lo[3], hi[3];
-        box_of(b, e, lo, hi);
-        // centroid bounds -> split axis
+    // object-median split of idx[b, e) on the longest centroid axis; returns mid
+    uint32_t split(uint32_t b, uint32_t e) {
         double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t j = b; j < e; ++j)
             for (int k = 0; k < 3; ++k) {
@@ -79,20 +65,78 @@ struct Builder {
             const double cx = c[3 * x + axis], cy = c[3 * y + axis];
             return cx < cy || (cx == cy && x < y);
         });
-        const uint32_t mid = b + (e - b) / 2;
-        const uint32_t left = node(b, mid, depth + 1);
-        const uint32_t right = node(mid, e, depth + 1);
-        // inflate by kPadK * M_b (M_b = max |coordinate|), round outward to f32
-        double m = 0.;
-        for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
-        const double pad = kPadKd * m + 1e-30;
-        float *N = &out->nodes[8 * static_cast<size_t>(id)];
-        for (int k = 0; k < 3; ++k) {
-            N[k] = down_f32(lo[k] - pad);
-            N[4 + k] = up_f32(hi[k] + pad);
+        return b + (e - b) / 2;
+    }
+
+    uint32_t leaf_record(uint32_t i) {
+        const uint32_t k = n_leaf++;
+        float *L = &out->leaves[8 * static_cast<size_t>(k)];
+        L[0] = static_cast<float>(c[3 * i]), L[1] = static_cast<float>(c[3 * i + 1]);
+        L[2] = static_cast<float>(c[3 * i + 2]), L[3] = r2p[i];
+        const double rr = r[i] * r[i];
+        L[4] = up_f32((2. * (static_cast<double>(r2p[i]) - rr)) * (1. + 1e-6));
+        L[5] = as_f32(i), L[6] = 0.f, L[7] = 0.f;
+        return k;
+    }
+
+    // Emits the 4-wide node over idx[b, e) (pre-order ids); returns its id. Up to
+    // 4 spheres become sphere children; more are cut into 4 parts by two levels
+    // of median splits, each part a sphere child (1 sphere) or an inner child.
+    uint32_t wide(uint32_t b, uint32_t e, uint32_t depth) {
+        out->depth = std::max(out->depth, depth);
+        std::vector<std::pair<uint32_t, uint32_t>> part;
+        if (e - b <= 4) {
+            for (uint32_t j = b; j < e; ++j) part.push_back({j, j + 1});
+        } else {
+            const uint32_t m = split(b, e);
+            const uint32_t m0 = split(b, m), m1 = split(m, e);
+            part = {{b, m0}, {m0, m}, {m, m1}, {m1, e}};
         }
-        N[3] = as_f32(left | (axis << 30));
-        N[7] = as_f32(right);
+        const uint32_t id = static_cast<uint32_t>(out->nodes.size() / 32);
+        out->nodes.resize(out->nodes.size() + 32, 0.f);
+        uint32_t ref[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+        double cen[4][3] = {};
+        float box[6][4];
+        for (int q = 0; q < 6; ++q)
+            for (int j = 0; j < 4; ++j) box[q][j] = INFINITY;  // empty slot (masked by its ref)
+        for (size_t j = 0; j < part.size(); ++j) {
+            double lo[3], hi[3];
+            bounds(part[j].first, part[j].second, lo, hi);
+            double m = 0.;
+            for (int k = 0; k < 3; ++k) m = std::max(m, std::max(std::fabs(lo[k]), std::fabs(hi[k])));
+            const double pad = kPadKd * m + 1e-30;
+            for (int k = 0; k < 3; ++k) {
+                box[2 * k][j] = down_f32(lo[k] - pad);
+                box[2 * k + 1][j] = up_f32(hi[k] + pad);
+                cen[j][k] = 0.5 * (lo[k] + hi[k]);
+            }
+        }
+        for (size_t j = 0; j < part.size(); ++j) {
+            const uint32_t pb = part[j].first, pe = part[j].second;
+            ref[j] = pe - pb == 1 ? (kSphereBit | leaf_record(idx[pb])) : wide(pb, pe, depth + 1);
+        }
+        // near-to-far child order per ray octant (bit k set: direction k < 0)
+        uint32_t ord[2] = {0, 0};
+        for (uint32_t o = 0; o < 8; ++o) {
+            int perm[4] = {0, 1, 2, 3};
+            std::stable_sort(perm, perm + 4, [&](int a, int b2) {
+                if ((ref[a] == kEmpty) != (ref[b2] == kEmpty)) return ref[b2] == kEmpty;
+                double ka = 0., kb = 0.;
+                for (int k = 0; k < 3; ++k) {
+                    const double s = (o >> k) & 1u ? -1. : 1.;
+                    ka += s * cen[a][k], kb += s * cen[b2][k];
+                }
+                return ka < kb;
+            });
+            uint32_t byte = 0;
+            for (int t = 0; t < 4; ++t) byte |= static_cast<uint32_t>(perm[t]) << (2 * t);
+            ord[o >> 2] |= byte << (8 * (o & 3));
+        }
+        float *N = &out->nodes[32 * static_cast<size_t>(id)];
+        for (int q = 0; q < 6; ++q)
+            for (int j = 0; j < 4; ++j) N[4 * q + j] = box[q][j];
+        for (int j = 0; j < 4; ++j) N[24 + j] = as_f32(ref[j]);
+        N[28] = as_f32(ord[0]), N[29] = as_f32(ord[1]), N[30] = 0.f, N[31] = 0.f;
         return id;
     }
 };
@@ -124,17 +168,12 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     }
     if (out.always.size() > kMaxAlways) return false;
     const uint32_t m = static_cast<uint32_t>(rest.size());
-    out.n_leaf = m;
-    out.n_inner = m ? m - 1 : 0;
-    out.nodes.assign(8 * static_cast<size_t>(out.n_inner), 0.f);
     out.leaves.assign(8 * static_cast<size_t>(m), 0.f);
-    if (m) {
-        Builder b{centers, radii, r2p, rest, &out};
-        b.n_inner = out.n_inner;
-        b.node(0, m, 1);
-        out.depth = b.max_depth;
-        if (out.depth > kMaxDepth) return false;
-    }
+    out.n_leaf = m;
+    if (m == 0) return true;
+    Builder b{centers, radii, r2p, rest, &out};
+    b.wide(0, m, 1);
+    out.n_node = static_cast<uint32_t>(out.nodes.size() / 32);
     return true;
 }
 

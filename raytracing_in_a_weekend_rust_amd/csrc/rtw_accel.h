@@ -48,14 +48,20 @@ constexpr float kPadK = 1.52587890625e-05f;  // 2^-16
 constexpr double kPadKd = 1.52587890625e-05;
 constexpr float kDirFloor = 9.094947017729282e-13f;  // 2^-40: |e_i| clamp before 1/e_i
 constexpr float kGuardBvh = 1e8f;       // |origin| beyond -> brute force for the segment
-constexpr uint32_t kMaxSpheres = 2048;  // 12-bit node ids (2n - 1 <= 4095)
-constexpr uint32_t kMaxDepth = 12;      // register stack: 3 x u64 of 16-bit entries
+constexpr uint32_t kMaxSpheres = 32768;  // 16-bit leaf / node ids
+constexpr uint32_t kStack = 16;          // register stack: 4 x u64 of 16-bit entries
+constexpr uint32_t kEmpty = 0xffffffffu;  // empty child slot
+constexpr uint32_t kSphereBit = 0x80000000u;  // child slot holds leaf (sphere) k
 constexpr uint32_t kMaxAlways = 16;
 constexpr uint32_t kMaxCand = 8;        // candidate list: 2 x u64 of 16-bit entries
 constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -> "always"
 
-// Node (32 B, two float4): {lo.xyz, left | axis << 30}, {hi.xyz, right}.
-// Child id < n_inner -> inner node; else leaf (id - n_inner) in leaf order.
+// Node (128 B, eight float4; 4-wide, children in the parent):
+//   q0..q5 = lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4] (padded boxes
+//   of the 4 children; an empty slot has every plane at +inf and is never hit),
+//   q6 = child refs (inner node id, kSphereBit | leaf k, or kEmpty),
+//   q7.x/.y = near-to-far child order per ray octant: byte o (octant bit k set
+//   = direction k negative) holds 4 2-bit slot indices, nearest first.
 // Leaf (32 B, two float4): {cx, cy, cz, R2'} (the pass-1 filter record) and
 // {d2, sphere index, 0, 0} with d2 >= 2 (R2' - r*r) (the filter's inflation, x2).
 
@@ -160,73 +166,110 @@ RTW_HD float sqrt32(float x) {
 #endif
 }
 
-// Collects the leaves (leaf-order ids) the walk cannot rule out. U (distance
-// units along e32) is the running cut; the caller seeds it from the "always"
-// spheres. Returns false on candidate-list overflow (caller brute-forces).
-// `visits` counts loop iterations (node or leaf tests).
+// One box slab test against the padded box of slot j (near distance out).
 template <typename F4>
-RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, uint32_t n_inner,
-                 const WalkRay &r, float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc,
-                 uint32_t &visits) {
-    uint64_t s0 = 0, s1 = 0, s2 = 0;
+RTW_HD bool slab_hit(float lox, float hix, float loy, float hiy, float loz, float hiz,
+                     const WalkRay &r, float U) {
+    const float t0x = fmaf(lox, r.ix, r.alx), t1x = fmaf(hix, r.ix, r.ahx);
+    const float t0y = fmaf(loy, r.iy, r.aly), t1y = fmaf(hiy, r.iy, r.ahy);
+    const float t0z = fmaf(loz, r.iz, r.alz), t1z = fmaf(hiz, r.iz, r.ahz);
+    const float nr = fmax3(fminf(t0x, t1x), fminf(t0y, t1y), fminf(t0z, t1z));
+    const float fr = fmin3(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fmaxf(t0z, t1z));
+    return !(nr > fr) && !(fr < r.tmin) && !(nr > U);
+}
+
+// The pass-1 filter on leaf k; a kept sphere joins the candidate list (false on
+// overflow) and, if it is a sure hit (disc beyond the filter's inflation + error,
+// far root clearly past tmin), its far root bounds the closest hit: U shrinks.
+template <typename F4>
+RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &r, float &U,
+                      uint64_t &c0, uint64_t &c1, uint32_t &nc) {
+    const F4 S = leaves[2 * k];
+    const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
+    const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
+    const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+    const float disc = fmaf(hb, hb, -cc);
+    if (disc < r.negG) return true;
+    if (nc >= kMaxCand) return false;
+    if (nc < 4) c0 |= static_cast<uint64_t>(k) << (16u * nc);
+    else c1 |= static_cast<uint64_t>(k) << (16u * (nc - 4u));
+    ++nc;
+    const float d2 = leaves[2 * k + 1].x;
+    if (disc > d2 - 2.f * r.negG) {
+        const float sd = sqrt32(disc);
+        const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
+        const float sfar = sd - hb;
+        const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
+        if (slo - slack > r.tmin * 1.001f) U = fminf(U, sfar + slack);
+    }
+    return true;
+}
+
+// Collects the leaves (leaf-order ids) the walk cannot rule out. Each iteration
+// takes one 4-wide node, tests its 4 child boxes, runs the leaf filter on hit
+// sphere children, continues with the nearest hit inner child and pushes the
+// other hit inner children (register stack, 16 entries). U (distance units along
+// e32) is the running cut; the caller seeds it from the "always" spheres.
+// Returns false on candidate-list or stack overflow (caller brute-forces).
+// `visits` counts loop iterations (node visits).
+template <typename F4>
+RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
+                 float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits) {
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     uint32_t sp = 0, cur = 0;
-    bool ok = true;
+    const uint32_t oct_shift = 8u * (r.neg & 3u);
+    const bool oct_hi = r.neg >= 4u;
     for (;;) {
         ++visits;
-        if (cur < n_inner) {
-            const F4 A = nodes[2 * cur], B = nodes[2 * cur + 1];
-            const float t0x = fmaf(A.x, r.ix, r.alx), t1x = fmaf(B.x, r.ix, r.ahx);
-            const float t0y = fmaf(A.y, r.iy, r.aly), t1y = fmaf(B.y, r.iy, r.ahy);
-            const float t0z = fmaf(A.z, r.iz, r.alz), t1z = fmaf(B.z, r.iz, r.ahz);
-            const float nr = fmax3(fminf(t0x, t1x), fminf(t0y, t1y), fminf(t0z, t1z));
-            const float fr = fmin3(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fmaxf(t0z, t1z));
-            if (!(nr > fr) && !(fr < r.tmin) && !(nr > U)) {
-                const uint32_t L = as_u32(A.w), R = as_u32(B.w);
-                const uint32_t lid = L & 0xffffu;
-                const bool right_first = (r.neg >> (L >> 30)) & 1u;
-                const uint32_t near_c = right_first ? R : lid, far_c = right_first ? lid : R;
-                s2 = (s2 << 16) | (s1 >> 48);
-                s1 = (s1 << 16) | (s0 >> 48);
-                s0 = (s0 << 16) | far_c;
-                ++sp;
-                cur = near_c;
-                continue;
-            }
-        } else {
-            const uint32_t k = cur - n_inner;
-            const F4 S = leaves[2 * k];
-            const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
-            const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
-            const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-            const float disc = fmaf(hb, hb, -cc);
-            if (!(disc < r.negG)) {
-                if (nc < kMaxCand) {
-                    if (nc < 4) c0 |= static_cast<uint64_t>(k) << (16u * nc);
-                    else c1 |= static_cast<uint64_t>(k) << (16u * (nc - 4u));
-                    ++nc;
-                } else {
-                    ok = false;
+        const F4 *N = nodes + 8u * cur;
+        const F4 qlx = N[0], qhx = N[1], qly = N[2], qhy = N[3], qlz = N[4], qhz = N[5], qc = N[6], qo = N[7];
+        uint32_t hit = 0;
+        hit |= slab_hit<F4>(qlx.x, qhx.x, qly.x, qhy.x, qlz.x, qhz.x, r, U) ? 1u : 0u;
+        hit |= slab_hit<F4>(qlx.y, qhx.y, qly.y, qhy.y, qlz.y, qhz.y, r, U) ? 2u : 0u;
+        hit |= slab_hit<F4>(qlx.z, qhx.z, qly.z, qhy.z, qlz.z, qhz.z, r, U) ? 4u : 0u;
+        hit |= slab_hit<F4>(qlx.w, qhx.w, qly.w, qhy.w, qlz.w, qhz.w, r, U) ? 8u : 0u;
+        const uint32_t ref[4] = {as_u32(qc.x), as_u32(qc.y), as_u32(qc.z), as_u32(qc.w)};
+        for (uint32_t j = 0; j < 4; ++j)
+            if (ref[j] == kEmpty) hit &= ~(1u << j);
+        // sphere children first: they may tighten U for the inner children
+        uint32_t smask = 0;
+        for (uint32_t j = 0; j < 4; ++j)
+            if ((hit >> j) & 1u && (ref[j] & kSphereBit)) smask |= 1u << j;
+        hit &= ~smask;
+        while (smask) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(smask));
+            smask &= smask - 1u;
+            if (!leaf_test(leaves, ref[j] & 0xffffu, r, U, c0, c1, nc)) return false;
+        }
+        // inner children, far to near: push all but the nearest, continue there
+        const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
+        uint32_t next = kEmpty;
+        for (int t = 3; t >= 0; --t) {
+            const uint32_t j = (ord >> (2 * t)) & 3u;
+            if ((hit >> j) & 1u) {
+                if (next != kEmpty) {
+                    if (sp >= kStack) return false;
+                    s3 = (s3 << 16) | (s2 >> 48);
+                    s2 = (s2 << 16) | (s1 >> 48);
+                    s1 = (s1 << 16) | (s0 >> 48);
+                    s0 = (s0 << 16) | next;
+                    ++sp;
                 }
-                // A sure hit (disc beyond the filter's inflation + error, far root
-                // clearly past tmin) bounds the closest hit by its far root.
-                const float d2 = leaves[2 * k + 1].x;
-                if (disc > d2 - 2.f * r.negG) {
-                    const float sd = sqrt32(disc);
-                    const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
-                    const float sfar = sd - hb;
-                    const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
-                    if (slo - slack > r.tmin * 1.001f) U = fminf(U, sfar + slack);
-                }
+                next = ref[j];
             }
         }
-        if (sp == 0) break;
-        cur = static_cast<uint32_t>(s0 & 0xffffu);
-        s0 = (s0 >> 16) | (s1 << 48);
-        s1 = (s1 >> 16) | (s2 << 48);
-        s2 >>= 16;
-        --sp;
+        if (next == kEmpty) {
+            if (sp == 0) break;
+            next = static_cast<uint32_t>(s0 & 0xffffu);
+            s0 = (s0 >> 16) | (s1 << 48);
+            s1 = (s1 >> 16) | (s2 << 48);
+            s2 = (s2 >> 16) | (s3 << 48);
+            s3 >>= 16;
+            --sp;
+        }
+        cur = next;
     }
-    return ok;
+    return true;
 }
 
 RTW_HD uint32_t cand_at(uint64_t c0, uint64_t c1, uint32_t j) {
@@ -254,8 +297,8 @@ inline float filter_r2p(const double *c, double rr) {
 // filter uses). Returns false if the scene is not eligible (n > kMaxSpheres or
 // too many "always" spheres): the kernel then scans by brute force.
 struct Bvh {
-    uint32_t n_inner = 0, n_leaf = 0, depth = 0;
-    std::vector<float> nodes;      // 8 floats per inner node (two float4)
+    uint32_t n_node = 0, n_leaf = 0, depth = 0;
+    std::vector<float> nodes;      // 32 floats per 4-wide node (eight float4)
     std::vector<float> leaves;     // 8 floats per leaf (two float4)
     std::vector<uint32_t> always;  // sphere indices tested exactly first, ascending
 };

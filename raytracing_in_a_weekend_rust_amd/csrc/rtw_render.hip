@@ -39,11 +39,17 @@
 namespace {
 
 constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
+// persistent phase 1: one workgroup per CU shares one LDS copy of the scene;
+// 768 threads = 3 waves per SIMD at the BVH kernel's ~160 VGPRs (1024 forces
+// 128 VGPRs and spills); RTW_PBLOCK=1024 selects the 4-wave build for A/B.
+constexpr int kPBlock = 768;
 constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
-constexpr size_t kLdsCap = 64 * 1024;     // dynamic LDS per workgroup
-constexpr int kCounters = 6;
+constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
+constexpr int kCounters = 7;
+constexpr double kBudgetX = 6.0;        // phase-1 segment budget per pixel, x samples per pixel
+constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 
 // Scene::hit strategies (one kernel instantiation each)
 constexpr int kScanF64 = 0;  // the reference's scan, f64 only
@@ -77,6 +83,13 @@ struct U128 {
     uint64_t lo, hi;
 };
 
+// Per-sphere shading record (48 B): the sphere's radius and its material row
+// flattened (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric).
+struct ShadeRec {
+    double r, a0, a1, a2, p;
+    uint32_t kind, _pad;
+};
+
 struct KParams {
     double p00[3], du[3], dv[3], from[3], ddu[3], ddv[3];
     double lat_dx[3], lat_dy[3], lat_pos0[3];  // lattice step (delta_v/s, delta_u/s) and pos0
@@ -84,22 +97,28 @@ struct KParams {
     uint32_t W, s, n_off, max_depth;
     uint32_t row_begin, row_step, n_rows, n_sph;
     uint32_t jump_bits, _pad;
-    uint32_t n_inner, n_leaf, n_always, _pad2;
+    uint32_t n_node, n_leaf, n_always, seg_budget;
+    uint32_t order, _pad3;
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
     const float4 *nodes;        // BVH inner nodes, 2 float4 each (rtw_accel.h)
     const float4 *leaves;       // BVH leaves, 2 float4 each
     const uint32_t *always;     // spheres tested exactly before the walk
-    const double *radius;       // r
-    const uint32_t *sph_mat;    // material row per sphere
-    const rtw_material *mats;   // material table
+    const ShadeRec *shade;      // per-sphere radius + material
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
     uint16_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
+    struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
+    uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
+    uint32_t *park_cursor;
+    U128 *seeds;                // per-pixel RNG children (persistent phase 1)
+    uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
+    uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
-                                   // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments
+                                   // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
+                                   // [6] parked pixels
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -208,13 +227,6 @@ struct PathStack {
 // Diagnostic build only (-DRTW_STAMPS, librtw_stamps.so): per-wave s_memtime
 // cycle sums per section; never compiled into the product library.
 #ifdef RTW_STAMPS
-#define STAMP_DECL uint64_t st_last = stamp_now(), st_acc[6] = {0, 0, 0, 0, 0, 0};
-#define STAMP(k)                                   \
-    do {                                           \
-        const uint64_t t_ = stamp_now();           \
-        st_acc[k] += t_ - st_last;                 \
-        st_last = t_;                              \
-    } while (0)
 __device__ __forceinline__ uint64_t stamp_now() {
     uint64_t t;
     __builtin_amdgcn_sched_barrier(0);
@@ -222,319 +234,473 @@ __device__ __forceinline__ uint64_t stamp_now() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
+struct Stamps {
+    uint64_t last = stamp_now(), acc[6] = {0, 0, 0, 0, 0, 0};
+};
+#define STAMP(k)                                   \
+    do {                                           \
+        const uint64_t t_ = stamp_now();           \
+        stp.acc[k] += t_ - stp.last;               \
+        stp.last = t_;                             \
+    } while (0)
 #else
-#define STAMP_DECL
+struct Stamps {};
 #define STAMP(k) \
     do {         \
     } while (0)
 #endif
 
 // ---------------------------------------------------------------- megakernel --
-template <bool kLds, int kMode>
-__global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
-    // LDS: exact f64 sphere records, then (BVH mode) the inner nodes and leaves.
-    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+// A pixel's sampling state between samples (camera.rs:354-374 loop state): the
+// pixel's RNG, the next lattice sample and the running sum.
+struct PixelState {
+    U128 rng;
+    uint32_t k;
+    double ar, ag, ab;
+};
+// Park queue entry: a pixel whose segment budget ran out at a sample boundary,
+// finished by the cooperative kernel (64 B).
+struct Parked {
+    uint32_t x, lr, k, _pad;
+    uint64_t rng_lo, rng_hi;
+    double ar, ag, ab, _pad2;
+};
+
+// Scene data a kernel reads per segment: f64 sphere records, shading records,
+// BVH nodes + leaves -- in LDS when they fit (kLds), else in HBM.
+struct SceneView {
+    const double4 *sph;
+    const ShadeRec *shd;
+    const float4 *nodes, *leaves;
+};
+// LDS layout: [n] double4 sph | [n] ShadeRec | (BVH) [8 n_node] + [2 n_leaf] float4
+__host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh) {
+    return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
+           (bvh ? (8 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
+}
+// One camera path in flight (the ray_color recursion flattened): the current
+// ray, its depth and the material rows of its non-dielectric bounces.
+struct Path {
+    double ox, oy, oz, dx, dy, dz;
+    uint32_t depth;
+    PathStack stk;
+};
+
+// get_ray, camera.rs:403: pixel_loc = (pixel00 + i*du) + j*dv
+struct PixelLoc {
+    double x, y, z;
+    PixelLoc() = default;
+    __device__ __forceinline__ PixelLoc(const KParams &P, uint32_t px, uint32_t py) {
+        const double fx = static_cast<double>(px), fy = static_cast<double>(py);
+        x = (P.p00[0] + P.du[0] * fx) + P.dv[0] * fy;
+        y = (P.p00[1] + P.du[1] * fx) + P.dv[1] * fy;
+        z = (P.p00[2] + P.du[2] * fx) + P.dv[2] * fy;
+    }
+};
+
+// camera.rs:400-420 + offset_lattice (422-450) + defocus_disk_sample (452-456):
+// the ray of lattice sample k; starts a fresh path.
+__device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, uint32_t k, U128 &rng,
+                                        Path &p) {
+    double offx, offy, offz;
+    if (P.s == 0) {
+        offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
+    } else {
+        const uint32_t ly = k / P.s, lx = k - ly * P.s;
+        const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
+        offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
+        offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
+        offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
+    }
+    const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
+    if (P.defocus_angle <= 0.) {
+        p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
+    } else {
+        double px, py;
+        do {  // vec3.rs:270-277: strict len^2 < 1
+            px = -1. + 2. * xs_next_01(rng);
+            py = -1. + 2. * xs_next_01(rng);
+        } while (!((px * px + py * py + 0. * 0.) < 1.));
+        p.ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
+        p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
+        p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
+    }
+    p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
+    p.depth = 0;
+    p.stk.clear();
+}
+
+// After Scene::hit: HitRecord + Material::scatter (materials.rs:22-111) on a hit,
+// the sky colour (camera.rs:395-397) on a miss. Returns true when the sample's
+// path ended (sky, or depth cap -> black); then (lr, lg, lb) is the leaf colour.
+__device__ __forceinline__ bool shade(const KParams &P, const double4 *__restrict__ sph,
+                                      const ShadeRec *__restrict__ shd, int best, double bt, double a,
+                                      Path &p, U128 &rng, uint64_t pix, uint64_t stride, double &lr,
+                                      double &lg, double &lb) {
+    lr = lg = lb = 0.;
+    if (best < 0) {
+        const double uy = p.dy / __builtin_sqrt(a);
+        const double t = 0.5 * (uy + 1.0);
+        const double om = 1.0 - t;
+        lr = om + 0.5 * t;
+        lg = om + 0.7 * t;
+        lb = om + t;
+        return true;
+    }
+    // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
+    const double4 S = sph[best];
+    const ShadeRec M = shd[best];
+    const double r = M.r;
+    const double px = p.dx * bt + p.ox, py = p.dy * bt + p.oy, pz = p.dz * bt + p.oz;
+    double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
+    const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
+    if (!front) nx = -nx, ny = -ny, nz = -nz;
+    double ndx, ndy, ndz;
+    if (M.kind != RTW_DIELECTRIC) {
+        // Lambertian and Metal each draw exactly one random_unit_vec and nothing
+        // else from the RNG: one rejection loop serves both (less divergence)
+        double ux, uy, uz;
+        random_unit_vec(rng, ux, uy, uz);
+        if (M.kind == RTW_LAMBERTIAN) {  // materials.rs:22-37
+            ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
+            if (ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = nx, ndy = ny, ndz = nz;
+        } else {  // Metal, materials.rs:52-63
+            const double l = __builtin_sqrt(a);
+            const double vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+            const double dt = vx * nx + vy * ny + vz * nz;
+            const double rx = vx - (nx * dt) * 2., ry = vy - (ny * dt) * 2., rz = vz - (nz * dt) * 2.;
+            ndx = rx + ux * M.p, ndy = ry + uy * M.p, ndz = rz + uz * M.p;
+        }
+        p.stk.push(static_cast<uint32_t>(best), P.spill, stride, pix);  // attenuation row
+    } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
+        const double ir = M.p;
+        const double ratio = front ? 1. / ir : ir;
+        const double l = __builtin_sqrt(a);
+        const double vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+        const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+        const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+        bool refl = ratio * sin_t > 1.;
+        if (!refl) {
+            double r0 = (1. - ir) / (1. + ir);
+            r0 = r0 * r0;
+            const double q = 1. - cos_t;
+            const double schlick = r0 + (1. - r0) * (q * ((q * q) * (q * q)));
+            refl = schlick > xs_next_01(rng);
+        }
+        if (refl) {  // vec3.rs:252-257
+            const double dt = vx * nx + vy * ny + vz * nz;
+            ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2., ndz = vz - (nz * dt) * 2.;
+        } else {  // vec3.rs:259-268
+            const double ct = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+            const double qx = (vx + nx * ct) * ratio, qy = (vy + ny * ct) * ratio,
+                         qz = (vz + nz * ct) * ratio;
+            const double w = -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
+            ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
+        }
+    }
+    p.ox = px, p.oy = py, p.oz = pz;
+    p.dx = ndx, p.dy = ndy, p.dz = ndz;
+    ++p.depth;
+    return p.depth >= P.max_depth;  // ray_color(depth >= max) -> black
+}
+
+// att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion associates
+// (camera.rs:389); then the sample's colour is added to the pixel sum.
+__device__ __forceinline__ void fold(const KParams &P, const ShadeRec *__restrict__ shd, Path &p,
+                                     uint64_t pix, uint64_t stride, double lr, double lg, double lb,
+                                     PixelState &ps) {
+    for (uint32_t j = p.stk.n; j-- > 0;) {
+        const ShadeRec &A = shd[p.stk.at(j, P.spill, stride, pix)];
+        lr = A.a0 * lr;
+        lg = A.a1 * lg;
+        lb = A.a2 * lb;
+    }
+    p.stk.clear();
+    ps.ar = ps.ar + lr, ps.ag = ps.ag + lg, ps.ab = ps.ab + lb;
+}
+
+// The reference's per-pixel loop: samples k.. of pixel (x, y) (ray_colors_lattice,
+// camera.rs:354-374) with the ray_color recursion (376-398) flattened into a
+// segment loop. `hit(ox, oy, oz, dx, dy, dz, a, bt) -> best` is the Scene::hit
+// strategy. Returns true if the pixel parked: `budget` segments were exceeded at
+// a sample boundary (ps then holds the state to resume from).
+template <class HitFn>
+__device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView &sv,
+                                              uint32_t x, uint32_t y, uint64_t pix, PixelState &ps,
+                                              uint32_t budget, uint32_t &seg, Stamps &stp, HitFn &&hit) {
+    const uint32_t n_off = P.n_off;
+    if (P.max_depth == 0) {  // every sample is black (no Scene::hit call)
+        ps.k = n_off;
+        return false;
+    }
+    if (ps.k >= n_off) return false;
+    const PixelLoc pl(P, x, y);
+    const uint64_t stride = static_cast<uint64_t>(P.n_rows) * P.W;
+    Path p;
+    gen_ray(P, pl, ps.k, ps.rng, p);
+    STAMP(0);  // 0: seed jump + pixel setup
+    for (;;) {
+        // ---- Scene::hit (hittable.rs:131-143): first minimum over all spheres ----
+        ++seg;
+        const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+        double bt = 0.;
+        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+        STAMP(1);
+        double lr, lg, lb;
+        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, lr, lg, lb);
+        STAMP(3);  // 3: hit record + scatter / sky
+        if (done) {
+            fold(P, sv.shd, p, pix, stride, lr, lg, lb, ps);
+            if (++ps.k >= n_off) break;
+            if (seg >= budget) return true;  // sample boundary: hand the rest to the coop kernel
+            gen_ray(P, pl, ps.k, ps.rng, p);
+        }
+        STAMP(4);  // 4: fold + next sample
+    }
+    return false;
+}
+
+__device__ __forceinline__ void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
+                                            const PixelState &ps) {
+    const double nf = static_cast<double>(P.n_off);
+    double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
+    o[0] = ps.ar / nf;
+    o[1] = ps.ag / nf;
+    o[2] = ps.ab / nf;
+}
+
+// Exact f64 Sphere::hit (sphere.rs:39-71) of sphere i against the current best,
+// keeping the lexicographic (t, index) minimum = the scan's first-minimum rule.
+__device__ __forceinline__ void exact_test(const double4 *__restrict__ sph, uint32_t i, double ox,
+                                           double oy, double oz, double dx, double dy, double dz,
+                                           double a, int &best, double &bt) {
+    const double4 S = sph[i];
+    double t;
+    if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t) &&
+        rtw_accel::better(t, i, bt, best)) {
+        bt = t;
+        best = static_cast<int>(i);
+    }
+}
+
+// f32 pass-1 state of one segment (shared by the filtered scan and the walk).
+// Exact-conservative filter: with ê = d/|d| the discriminant's sign is that of
+// D' = (OC.ê)^2 - (|OC|^2 - R2) = D / a. Computed in f32 with oc = o32 - c32,
+// e = fl32(ê), and R2' >= R2 + K (m_c^2 + R2/2) in place of R2 (host, rounded
+// up), a first-order bound of the f32 error is  u32 (81 M^2 + 4 R2') with
+// M_i = |o_i| + |c_i|, M^2 <= 2 (m_o^2 + m_c^2); K = 512 u32 then leaves
+//   disc32 >= D' - K m_o^2 - (floor)
+// so every sphere whose f64 discriminant is >= 0 (or NaN) passes the test
+// disc32 >= -G, G = K m_o^2 + floor. NaN/inf anywhere -> kept.
+struct Seg32 {
+    float ox, oy, oz, ex, ey, ez, negG;
+    double mo, sa;
+    bool fast;
+    __device__ __forceinline__ Seg32(double x, double y, double z, double dx, double dy, double dz,
+                                     double a, bool filter) {
+        mo = fmax(fmax(__builtin_fabs(x), __builtin_fabs(y)), __builtin_fabs(z));
+        fast = filter && mo <= kGuardHi;  // false for NaN too
+        sa = __builtin_sqrt(a);
+        const double inv = 1.0 / sa;
+        ex = static_cast<float>(dx * inv), ey = static_cast<float>(dy * inv), ez = static_cast<float>(dz * inv);
+        ox = static_cast<float>(x), oy = static_cast<float>(y), oz = static_cast<float>(z);
+        negG = rtw_accel::filter_neg_g(mo);
+    }
+    __device__ __forceinline__ bool pass(const float4 S) const {
+        const float ocx = ox - S.x, ocy = oy - S.y, ocz = oz - S.z;
+        const float hb = fmaf(ocx, ex, fmaf(ocy, ey, ocz * ez));
+        const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
+        const float disc = fmaf(hb, hb, -cc);
+        return !(disc < negG);
+    }
+};
+
+// Counters kept per lane, atomically added at the end of a kernel.
+struct Tally {
+    uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0, parked = 0, witer = 0;
+};
+
+// The scan: every sphere in index order (first = lane's sub-range start, step =
+// sphere stride for cooperative groups); pass 1 = f32 filter on wave-uniform
+// records, pass 2 = f64 on the lane's candidates in index order.
+__device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restrict__ sph,
+                                        const Seg32 &g, double ox, double oy, double oz, double dx,
+                                        double dy, double dz, double a, double &bt, Tally &tl) {
     const uint32_t n = P.n_sph;
-    const double4 *__restrict__ sph = P.sph;
-    const float4 *__restrict__ nodes = P.nodes;
-    const float4 *__restrict__ leaves = P.leaves;
+    const uint32_t lane = threadIdx.x & 63u;
+    int best = -1;
+    for (uint32_t base = 0; base < n; base += kChunk) {
+        const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
+        // sphere base+j is bit (31 - j): highest set bit = lowest index
+        uint32_t mask;
+        if (g.fast) {
+            mask = 0;
+            for (uint32_t q = 0; q < static_cast<uint32_t>(kChunk); q += kGroup) {
+#pragma unroll
+                for (int j = 0; j < kGroup; ++j)
+                    mask = mask + mask + static_cast<uint32_t>(g.pass(ld_filt(P.filt, base + q + j)));
+            }
+            if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
+        } else {
+            mask = cnt == static_cast<uint32_t>(kChunk) ? ~0u : ~((1u << (kChunk - cnt)) - 1u);
+        }
+        while (mask) {
+            {  // the wave's first active lane counts the wave-level iteration
+                const uint64_t exm = __builtin_amdgcn_read_exec();
+                tl.nwave2 += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
+            }
+            const uint32_t top = 31u - static_cast<uint32_t>(__builtin_clz(mask));
+            mask ^= 1u << top;
+            ++tl.ntest;
+            exact_test(sph, base + (31u - top), ox, oy, oz, dx, dy, dz, a, best, bt);
+        }
+    }
+    return best;
+}
+
+// Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
+// exact candidates, the cut check; anything unproven falls back to the scan.
+__device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restrict__ sph,
+                                       const float4 *__restrict__ nodes,
+                                       const float4 *__restrict__ leaves, double ox, double oy,
+                                       double oz, double dx, double dy, double dz, double a,
+                                       double &bt, Tally &tl) {
+    const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
+    int best = -1;
+    bool brute = !g.fast;
+    if (g.fast) {
+        for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
+            const uint32_t i = ld_const_u32(P.always, j);
+            if (g.pass(ld_filt(P.filt, i))) {
+                ++tl.ntest;
+                exact_test(sph, i, ox, oy, oz, dx, dy, dz, a, best, bt);
+            }
+        }
+        rtw_accel::WalkRay wr;
+        if (P.n_leaf == 0) {
+        } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
+            brute = true;
+        } else {
+            float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
+            uint64_t c0 = 0, c1 = 0;
+            uint32_t nc = 0;
+            if (!rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits)) {
+                brute = true;
+            } else {
+                for (uint32_t j = 0; j < nc; ++j) {
+                    const uint32_t leaf = rtw_accel::cand_at(c0, c1, j);
+                    ++tl.ntest;
+                    exact_test(sph, __float_as_uint(leaves[2u * leaf + 1u].y), ox, oy, oz, dx, dy, dz,
+                               a, best, bt);
+                }
+                brute = !rtw_accel::cut_ok(U, best, bt, g.sa);
+            }
+        }
+    }
+    if (brute) {
+        ++tl.nbrute;
+        best = scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
+    }
+    return best;
+}
+
+__device__ __forceinline__ void flush_tally(const KParams &P, const Tally &tl, bool wave_iters) {
+    if (!P.counters) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (tl.seg) atomicAdd(&P.counters[0], static_cast<unsigned long long>(tl.seg));
+    if (wave_iters) {  // one-lane-per-pixel kernel: the wave's trip count = max over lanes
+        uint32_t m = tl.seg;
+        for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
+        if (lane == 0 && m) atomicAdd(&P.counters[1], static_cast<unsigned long long>(m));
+    }
+    if (tl.ntest) atomicAdd(&P.counters[2], static_cast<unsigned long long>(tl.ntest));
+    if (tl.nwave2) atomicAdd(&P.counters[3], static_cast<unsigned long long>(tl.nwave2));
+    if (tl.witer) atomicAdd(&P.counters[1], static_cast<unsigned long long>(tl.witer));
+    if (tl.visits) atomicAdd(&P.counters[4], static_cast<unsigned long long>(tl.visits));
+    if (tl.nbrute) atomicAdd(&P.counters[5], static_cast<unsigned long long>(tl.nbrute));
+    if (tl.parked) atomicAdd(&P.counters[6], static_cast<unsigned long long>(tl.parked));
+}
+
+template <bool kLds, int kMode>
+__device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds) {
+    SceneView v{P.sph, P.shade, P.nodes, P.leaves};
     if (kLds) {
-        for (uint32_t i = threadIdx.x; i < n; i += kBlock) lds_sph[i] = P.sph[i];
-        float4 *lf = reinterpret_cast<float4 *>(lds_sph + n);
+        const uint32_t n = P.n_sph;
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = P.sph[i];
+        ShadeRec *ls = reinterpret_cast<ShadeRec *>(lds + n);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
+        float4 *lf = reinterpret_cast<float4 *>(ls + n);
         if (kMode == kBvh) {
-            const uint32_t nn = 2u * P.n_inner, nl = 2u * P.n_leaf;
-            for (uint32_t i = threadIdx.x; i < nn; i += kBlock) lf[i] = P.nodes[i];
-            for (uint32_t i = threadIdx.x; i < nl; i += kBlock) lf[nn + i] = P.leaves[i];
+            const uint32_t nn = 8u * P.n_node, nl = 2u * P.n_leaf;
+            for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lf[i] = P.nodes[i];
+            for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) lf[nn + i] = P.leaves[i];
         }
         __syncthreads();
-        sph = lds_sph;
-        nodes = lf;
-        leaves = lf + 2u * P.n_inner;
+        v.sph = lds;
+        v.shd = ls;
+        v.nodes = lf;
+        v.leaves = lf + 8u * P.n_node;
     }
-    const float4 *filt = P.filt;
+    return v;
+}
+
+// Phase 1: one lane per pixel (16x16 tiles). With a segment budget, pixels that
+// exceed it at a sample boundary park in P.park for rtw_finish_parked.
+template <bool kLds, int kMode>
+__global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
+    const double4 *sph = sv.sph;
+    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
 
     const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
     const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
-    uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0;
-    const uint32_t lane = threadIdx.x & 63u;
-    STAMP_DECL
+    Tally tl;
+    Stamps stp;
 
     if (x < P.W && lr < P.n_rows) {
         const uint32_t y = P.row_begin + lr * P.row_step;
-        U128 rng = child_of(jump_state(U128{P.seed_lo, P.seed_hi},
-                                       static_cast<uint64_t>(y) * P.W + x, P.jump, P.jump_bits));
-
-        // get_ray, camera.rs:403: (pixel00 + i*du) + j*dv
-        const double fx = static_cast<double>(x), fy = static_cast<double>(y);
-        const double plx = (P.p00[0] + P.du[0] * fx) + P.dv[0] * fy;
-        const double ply = (P.p00[1] + P.du[1] * fx) + P.dv[1] * fy;
-        const double plz = (P.p00[2] + P.du[2] * fx) + P.dv[2] * fy;
-
-        double ox, oy, oz, dx, dy, dz;
-        // camera.rs:400-420 + offset_lattice (422-450) + defocus_disk_sample (452-456)
-        auto gen_ray = [&](uint32_t k) {
-            double offx, offy, offz;
-            if (P.s == 0) {
-                offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
+        PixelState ps;
+        ps.rng = child_of(jump_state(U128{P.seed_lo, P.seed_hi}, static_cast<uint64_t>(y) * P.W + x,
+                                     P.jump, P.jump_bits));
+        ps.k = 0;
+        ps.ar = ps.ag = ps.ab = 0.;
+        const uint64_t pix = static_cast<uint64_t>(lr) * P.W + x;  // spill column
+        auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                       double &bt) -> int {
+            if constexpr (kMode == kBvh) {
+                return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
             } else {
-                const uint32_t ly = k / P.s, lx = k - ly * P.s;
-                const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
-                offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
-                offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
-                offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
+                const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
+                return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
             }
-            const double sx = plx + offx, sy = ply + offy, sz = plz + offz;
-            if (P.defocus_angle <= 0.) {
-                ox = P.from[0], oy = P.from[1], oz = P.from[2];
-            } else {
-                double px, py;
-                do {  // vec3.rs:270-277: strict len^2 < 1
-                    px = -1. + 2. * xs_next_01(rng);
-                    py = -1. + 2. * xs_next_01(rng);
-                } while (!((px * px + py * py + 0. * 0.) < 1.));
-                ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
-                oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
-                oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
-            }
-            dx = sx - ox, dy = sy - oy, dz = sz - oz;
         };
-
-        double accr = 0., accg = 0., accb = 0.;
-        const uint32_t n_off = P.n_off;
-        if (P.max_depth == 0) {  // every sample is black, RNG still consumed by get_ray
-            for (uint32_t k = 0; k < n_off; ++k) gen_ray(k);
+        if (trace_samples(P, sv, x, y, pix, ps, P.seg_budget, tl.seg, stp, hit)) {
+            const uint32_t slot = atomicAdd(P.park_count, 1u);
+            Parked q;
+            q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
+            q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
+            q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
+            P.park[slot] = q;
+            ++tl.parked;
         } else {
-            PathStack stk;
-            const uint64_t pix = static_cast<uint64_t>(lr) * P.W + x;  // spill column
-            const uint64_t stride = static_cast<uint64_t>(P.n_rows) * P.W;
-            uint32_t depth = 0, k = 0;
-            gen_ray(0);
-            STAMP(0);  // 0: seed jump + pixel setup
-            for (;;) {
-                // ---- Scene::hit (hittable.rs:131-143): first minimum over all spheres ----
-                ++seg;
-                const double a = dx * dx + dy * dy + dz * dz;
-                int best = -1;
-                double bt = 0.;
-
-                // ---- f32 setup shared by the filter and the walk: unit direction e,
-                // per-lane margin G ----
-                // Exact-conservative filter. With ê = d/|d| the discriminant's sign is
-                // that of D' = (OC.ê)^2 - (|OC|^2 - R2) = D / a. Computed in f32 with
-                // oc = o32 - c32, e = fl32(ê), and R2' >= R2 + K (m_c^2 + R2/2) in
-                // place of R2 (host, rounded up), a first-order bound of the f32
-                // error is  u32 (81 M^2 + 4 R2') with M_i = |o_i| + |c_i|,
-                // M^2 <= 2 (m_o^2 + m_c^2); K = 512 u32 then leaves
-                //   disc32 >= D' - K m_o^2 - (floor)
-                // so every sphere whose f64 discriminant is >= 0 (or NaN) passes the
-                // test disc32 >= -G, G = K m_o^2 + floor. NaN/inf anywhere -> kept.
-                const double mo64 = fmax(fmax(__builtin_fabs(ox), __builtin_fabs(oy)), __builtin_fabs(oz));
-                const bool fast = kMode != kScanF64 && mo64 <= kGuardHi;  // false for NaN too
-                const double sa = __builtin_sqrt(a);
-                const double inv = 1.0 / sa;
-                const float ex = static_cast<float>(dx * inv), ey = static_cast<float>(dy * inv),
-                            ez = static_cast<float>(dz * inv);
-                const float o32x = static_cast<float>(ox), o32y = static_cast<float>(oy),
-                            o32z = static_cast<float>(oz);
-                const float negG = rtw_accel::filter_neg_g(mo64);
-
-                // exact f64 Sphere::hit (sphere.rs:39-71) of sphere i; keeps the
-                // lexicographic (t, index) minimum = the scan's first-minimum rule
-                auto exact = [&](uint32_t i) {
-                    ++ntest;
-                    const double4 S = sph[i];
-                    double t;
-                    if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t) &&
-                        rtw_accel::better(t, i, bt, best)) {
-                        bt = t;
-                        best = static_cast<int>(i);
-                    }
-                };
-                // f32 filter value for one pass-1 record (wave-uniform SGPR operand)
-                auto filt_pass = [&](const float4 S) {
-                    const float ocx = o32x - S.x, ocy = o32y - S.y, ocz = o32z - S.z;
-                    const float hb = fmaf(ocx, ex, fmaf(ocy, ey, ocz * ez));
-                    const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-                    const float disc = fmaf(hb, hb, -cc);
-                    return !(disc < negG);
-                };
-                // The scan: every sphere in index order, pass 1 (f32 filter, wave-
-                // uniform) then pass 2 (f64, per lane, the lane's candidates only).
-                auto scan = [&](bool use_filter) {
-                    best = -1;
-                    for (uint32_t base = 0; base < n; base += kChunk) {
-                        const uint32_t cnt = n - base < static_cast<uint32_t>(kChunk) ? n - base : kChunk;
-                        // sphere base+j is bit (31 - j): highest set bit = lowest index
-                        uint32_t mask;
-                        if (use_filter) {
-                            mask = 0;
-                            for (uint32_t g = 0; g < static_cast<uint32_t>(kChunk); g += kGroup) {
-#pragma unroll
-                                for (int j = 0; j < kGroup; ++j)
-                                    mask = mask + mask + static_cast<uint32_t>(filt_pass(ld_filt(filt, base + g + j)));
-                            }
-                            if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
-                        } else {
-                            mask = cnt == static_cast<uint32_t>(kChunk) ? ~0u : ~((1u << (kChunk - cnt)) - 1u);
-                        }
-                        STAMP(1);  // 1: pass 1 (f32 filter)
-                        while (mask) {
-                            {  // the wave's first active lane counts the wave-level iteration
-                                const uint64_t exm = __builtin_amdgcn_read_exec();
-                                nwave2 += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
-                            }
-                            const uint32_t top = 31u - static_cast<uint32_t>(__builtin_clz(mask));
-                            mask ^= 1u << top;
-                            exact(base + (31u - top));
-                        }
-                        STAMP(2);  // 2: pass 2 (exact f64 tests)
-                    }
-                };
-
-                if constexpr (kMode == kBvh) {
-                    bool brute = !fast;
-                    if (fast) {
-                        for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
-                            const uint32_t i = ld_const_u32(P.always, j);
-                            if (filt_pass(ld_filt(filt, i))) exact(i);
-                        }
-                        rtw_accel::WalkRay wr;
-                        if (P.n_leaf == 0) {
-                        } else if (!rtw_accel::walk_setup(o32x, o32y, o32z, ex, ey, ez, mo64, sa, negG, wr)) {
-                            brute = true;
-                        } else {
-                            float U = best >= 0 ? rtw_accel::seed_cut(bt, sa) : INFINITY;
-                            uint64_t c0 = 0, c1 = 0;
-                            uint32_t nc = 0;
-                            if (!rtw_accel::walk(nodes, leaves, P.n_inner, wr, U, c0, c1, nc, visits)) {
-                                brute = true;
-                            } else {
-                                for (uint32_t j = 0; j < nc; ++j) {
-                                    const uint32_t leaf = rtw_accel::cand_at(c0, c1, j);
-                                    exact(__float_as_uint(leaves[2u * leaf + 1u].y));
-                                }
-                                brute = !rtw_accel::cut_ok(U, best, bt, sa);
-                            }
-                        }
-                    }
-                    if (brute) {
-                        ++nbrute;
-                        scan(fast);
-                    }
-                    STAMP(1);
-                } else {
-                    scan(fast);
-                }
-
-                bool finish;
-                double lr_ = 0., lg = 0., lb = 0.;
-                if (best >= 0) {
-                    // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
-                    const double4 S = sph[best];
-                    const double r = P.radius[best];
-                    const double px = dx * bt + ox, py = dy * bt + oy, pz = dz * bt + oz;
-                    double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
-                    const bool front = (dx * nx + dy * ny + dz * nz) < 0.;
-                    if (!front) nx = -nx, ny = -ny, nz = -nz;
-                    const uint32_t mi = P.sph_mat[best];
-                    const rtw_material M = P.mats[mi];
-                    double ndx, ndy, ndz;
-                    if (M.kind == RTW_LAMBERTIAN) {  // materials.rs:22-37
-                        double ux, uy, uz;
-                        random_unit_vec(rng, ux, uy, uz);
-                        ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
-                        if (ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = nx, ndy = ny, ndz = nz;
-                        stk.push(mi, P.spill, stride, pix);
-                    } else if (M.kind == RTW_METAL) {  // materials.rs:52-63
-                        const double l = __builtin_sqrt(a);
-                        const double vx = dx / l, vy = dy / l, vz = dz / l;
-                        const double dt = vx * nx + vy * ny + vz * nz;
-                        const double rx = vx - (nx * dt) * 2., ry = vy - (ny * dt) * 2.,
-                                     rz = vz - (nz * dt) * 2.;
-                        double ux, uy, uz;
-                        random_unit_vec(rng, ux, uy, uz);
-                        ndx = rx + ux * M.fuzz, ndy = ry + uy * M.fuzz, ndz = rz + uz * M.fuzz;
-                        stk.push(mi, P.spill, stride, pix);
-                    } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
-                        const double ratio = front ? 1. / M.ir : M.ir;
-                        const double l = __builtin_sqrt(a);
-                        const double vx = dx / l, vy = dy / l, vz = dz / l;
-                        const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
-                        const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
-                        bool refl = ratio * sin_t > 1.;
-                        if (!refl) {
-                            double r0 = (1. - M.ir) / (1. + M.ir);
-                            r0 = r0 * r0;
-                            const double q = 1. - cos_t;
-                            const double schlick = r0 + (1. - r0) * (q * ((q * q) * (q * q)));
-                            refl = schlick > xs_next_01(rng);
-                        }
-                        if (refl) {  // vec3.rs:252-257
-                            const double dt = vx * nx + vy * ny + vz * nz;
-                            ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2.,
-                            ndz = vz - (nz * dt) * 2.;
-                        } else {  // vec3.rs:259-268
-                            const double ct = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
-                            const double qx = (vx + nx * ct) * ratio, qy = (vy + ny * ct) * ratio,
-                                         qz = (vz + nz * ct) * ratio;
-                            const double w =
-                                -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
-                            ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
-                        }
-                    }
-                    ox = px, oy = py, oz = pz;
-                    dx = ndx, dy = ndy, dz = ndz;
-                    ++depth;
-                    finish = depth >= P.max_depth;  // ray_color(depth >= max) -> black
-                } else {
-                    // sky, camera.rs:395-397
-                    const double uy = dy / __builtin_sqrt(a);
-                    const double t = 0.5 * (uy + 1.0);
-                    const double om = 1.0 - t;
-                    lr_ = om + 0.5 * t;
-                    lg = om + 0.7 * t;
-                    lb = om + t;
-                    finish = true;
-                }
-
-                STAMP(3);  // 3: hit record + scatter / sky
-                if (finish) {
-                    // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion
-                    for (uint32_t j = stk.n; j-- > 0;) {
-                        const rtw_material &A = P.mats[stk.at(j, P.spill, stride, pix)];
-                        lr_ = A.albedo[0] * lr_;
-                        lg = A.albedo[1] * lg;
-                        lb = A.albedo[2] * lb;
-                    }
-                    stk.clear();
-                    accr = accr + lr_, accg = accg + lg, accb = accb + lb;
-                    if (++k >= n_off) break;
-                    depth = 0;
-                    gen_ray(k);
-                }
-                STAMP(4);  // 4: fold + next sample
-            }
+            write_pixel(P, x, lr, ps);
         }
-        const double nf = static_cast<double>(n_off);
-        double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
-        o[0] = accr / nf;
-        o[1] = accg / nf;
-        o[2] = accb / nf;
     }
 
-    // segments (atomic, wave-reduced by the compiler) and the wave's trip count
 #ifdef RTW_STAMPS
     {  // max over lanes of each section sum -> one row per wave
+        const uint32_t lane = threadIdx.x & 63u;
         uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.y) * gridDim.x * 4 + blockIdx.x * 4 + threadIdx.x / 64u) * 8;
         for (int k = 0; k < 6; ++k) {
-            uint64_t v = st_acc[k];
+            uint64_t v = stp.acc[k];
             for (int off = 32; off > 0; off >>= 1) {
                 const uint64_t o = __shfl_xor(v, off);
                 v = v > o ? v : o;
             }
             if (lane == 0) row[k] = v;
         }
-        uint64_t sm = seg;
+        uint64_t sm = tl.seg;
         for (int off = 32; off > 0; off >>= 1) {
             const uint64_t o = __shfl_xor(sm, off);
             sm = sm > o ? sm : o;
@@ -542,16 +708,207 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         if (lane == 0) row[6] = sm, row[7] = stamp_now();
     }
 #endif
-    if (P.counters) {
-        if (seg) atomicAdd(&P.counters[0], static_cast<unsigned long long>(seg));
-        uint32_t m = seg;
-        for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), off)));
-        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&P.counters[1], static_cast<unsigned long long>(m));
-        if (ntest) atomicAdd(&P.counters[2], static_cast<unsigned long long>(ntest));
-        if (nwave2) atomicAdd(&P.counters[3], static_cast<unsigned long long>(nwave2));
-        if (visits) atomicAdd(&P.counters[4], static_cast<unsigned long long>(visits));
-        if (nbrute) atomicAdd(&P.counters[5], static_cast<unsigned long long>(nbrute));
+    flush_tally(P, tl, true);
+}
+
+// Per-pixel RNG children (copy_reset, camera.rs:269-272) of the shard's pixels, in
+// shard order, by device jump-ahead: the persistent kernel refills lanes from it.
+__global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+    if (i >= npix) return;
+    const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
+    const uint32_t y = P.row_begin + lr * P.row_step;
+    P.seeds[i] = child_of(jump_state(U128{P.seed_lo, P.seed_hi}, static_cast<uint64_t>(y) * P.W + x,
+                                     P.jump, P.jump_bits));
+}
+
+// Phase 1, persistent form: every lane runs one pixel at a time and, when the
+// pixel completes (or parks at the segment budget), takes the next pixel of the
+// shard from a global cursor (one atomic per wave per refill). Waves stay full
+// until the cursor runs dry, so the launch ends within about one pixel's
+// duration of the last pixel handed out.
+template <bool kLds, int kMode, int kThreads>
+__global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
+    const double4 *sph = sv.sph;
+    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
+    Tally tl;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+    const uint64_t stride = npix;
+    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                   double &bt) -> int {
+        if constexpr (kMode == kBvh) {
+            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
+        } else {
+            const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
+            return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
+        }
+    };
+    bool need = true;
+    uint32_t x = 0, lr = 0, pseg = 0;
+    uint64_t pix = 0;
+    PixelState ps;
+    Path p;
+    PixelLoc pl;
+    for (;;) {
+        {  // the wave's first active lane counts the wave-level iteration
+            const uint64_t exm = __builtin_amdgcn_read_exec();
+            tl.witer += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
+        }
+        if (need) {  // refill: one atomic for all lanes of the wave that need a pixel
+            const uint64_t m = __ballot(1);
+            const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+            uint32_t base = 0;
+            if (rank == 0) base = atomicAdd(P.pix_cursor, static_cast<uint32_t>(__popcll(m)));
+            base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
+            const uint64_t ticket = static_cast<uint64_t>(base) + rank;
+            if (ticket >= npix) break;
+            // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
+            // cheapest in the book's scenes, go last and fill the drain)
+            const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
+            x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
+            lr = P.order ? P.n_rows - 1u - tr : tr;
+            pix = static_cast<uint64_t>(lr) * P.W + x;
+            ps.rng = P.seeds[pix];
+            ps.k = 0;
+            ps.ar = ps.ag = ps.ab = 0.;
+            pseg = 0;
+            if (P.max_depth == 0) {  // every sample black, no Scene::hit call
+                ps.k = P.n_off;
+                write_pixel(P, x, lr, ps);
+                continue;
+            }
+            pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
+            gen_ray(P, pl, 0, ps.rng, p);
+            need = false;
+        }
+        ++tl.seg, ++pseg;
+        const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+        double bt = 0.;
+        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+        double cr, cg, cb;
+        if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, cr, cg, cb)) {
+            fold(P, sv.shd, p, pix, stride, cr, cg, cb, ps);
+            const bool done = ++ps.k >= P.n_off;
+            if ((done || pseg >= P.seg_budget) && P.diag) {
+                P.diag[2 * pix] = pseg;
+                P.diag[2 * pix + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+            }
+            if (done) {
+                write_pixel(P, x, lr, ps);
+                need = true;
+            } else if (pseg >= P.seg_budget) {  // park at the sample boundary
+                const uint32_t slot = atomicAdd(P.park_count, 1u);
+                Parked q;
+                q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
+                q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
+                q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
+                P.park[slot] = q;
+                ++tl.parked;
+                need = true;
+            } else {
+                gen_ray(P, pl, ps.k, ps.rng, p);
+            }
+        }
     }
+    flush_tally(P, tl, false);
+}
+
+// (t, index) minimum across a group of `kG` lanes (16 or 64): DPP butterflies
+// inside each row of 16 (xor 1, xor 2, half-row mirror, row mirror), then
+// cross-row exchanges. Every lane of the group ends with the same result.
+template <int kCtrl>
+__device__ __forceinline__ void dpp_min_step(double &bt, int &best) {
+    const int ob = __builtin_amdgcn_update_dpp(-1, best, kCtrl, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(bt), kCtrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(bt), kCtrl, 0xf, 0xf, false);
+    const double ot = __hiloint2double(hi, lo);
+    if (ob >= 0 && rtw_accel::better(ot, static_cast<uint32_t>(ob), bt, best)) bt = ot, best = ob;
+}
+__device__ __forceinline__ void shfl_min_step(double &bt, int &best, int off) {
+    const int ob = __shfl_xor(best, off);
+    const double ot = __shfl_xor(bt, off);
+    if (ob >= 0 && rtw_accel::better(ot, static_cast<uint32_t>(ob), bt, best)) bt = ot, best = ob;
+}
+template <uint32_t kG>
+__device__ __forceinline__ void group_min(double &bt, int &best) {
+    dpp_min_step<0xB1>(bt, best);   // quad_perm [1,0,3,2]
+    dpp_min_step<0x4E>(bt, best);   // quad_perm [2,3,0,1]
+    dpp_min_step<0x141>(bt, best);  // row_half_mirror
+    dpp_min_step<0x140>(bt, best);  // row_mirror
+    if (kG >= 32) shfl_min_step(bt, best, 16);
+    if (kG >= 64) shfl_min_step(bt, best, 32);
+}
+
+// Phase 2: the parked pixels, kG lanes per pixel. Persistent groups take pixels
+// in park order (the heaviest parked first) from an atomic cursor. Scene::hit is
+// split across the group: lane j filters spheres j, j + kG, ... against the
+// LDS-staged pass-1 records, runs the exact f64 test on its candidates, then
+// the group takes the (t, index) minimum. Every lane of a group then runs the
+// identical scatter on the identical RNG state.
+template <bool kLds, uint32_t kG>
+__global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
+    const double4 *sph = sv.sph;
+    const uint32_t n = P.n_sph;
+    const float4 *filt = P.filt;
+    if (kLds) {  // pass-1 records after the shading records
+        float4 *lf = reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + n);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lf[i] = P.filt[i];
+        __syncthreads();
+        filt = lf;
+    }
+    const uint32_t sub = threadIdx.x & (kG - 1u);
+    Tally tl;
+    uint32_t seg = 0;
+    for (;;) {
+        uint32_t item = 0;
+        if (sub == 0) item = atomicAdd(P.park_cursor, 1u);
+        item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
+        if (item >= *P.park_count) break;
+        const Parked q = P.park[item];
+        const uint32_t y = P.row_begin + q.lr * P.row_step;
+        PixelState ps;
+        ps.rng = U128{q.rng_lo, q.rng_hi};
+        ps.k = q.k;
+        ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
+        const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
+        auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                       double &bt) -> int {
+            const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
+            int best = -1;
+            bt = 0.;
+            for (uint32_t base = 0; base < n; base += 32u * kG) {
+                uint32_t mask = 0;  // bit j: sphere base + sub + j*kG is a candidate
+#pragma unroll 8
+                for (uint32_t j = 0; j < 32u; ++j) {
+                    const uint32_t i = base + sub + j * kG;
+                    if (i < n && (!g.fast || g.pass(filt[i]))) mask |= 1u << j;
+                }
+                while (mask) {
+                    const uint32_t j = static_cast<uint32_t>(__builtin_ctz(mask));
+                    mask &= mask - 1u;
+                    ++tl.ntest;
+                    exact_test(sph, base + sub + j * kG, ox, oy, oz, dx, dy, dz, a, best, bt);
+                }
+            }
+            group_min<kG>(bt, best);
+            return best;
+        };
+        uint32_t s = 0;
+        Stamps stp;
+        trace_samples(P, sv, q.x, y, pix, ps, 0xffffffffu, s, stp, hit);
+        if (sub == 0) {
+            write_pixel(P, q.x, q.lr, ps);
+            seg += s;
+        }
+    }
+    tl.seg = seg;
+    flush_tally(P, tl, false);
 }
 
 // ------------------------------------------------------------------- probes --
@@ -589,19 +946,24 @@ struct rtw_session {
     hipStream_t own = nullptr;
     double4 *d_sph = nullptr;
     float4 *d_filt = nullptr;
-    double *d_rad = nullptr;
-    uint32_t *d_smat = nullptr;
-    rtw_material *d_mats = nullptr;
+    ShadeRec *d_shade = nullptr;
     uint4 *d_jump = nullptr;
     unsigned long long *d_counters = nullptr;
     uint16_t *d_spill = nullptr;
     size_t spill_bytes = 0;
+    Parked *d_park = nullptr;  // park queue, one slot per pixel of the largest shard so far
+    size_t park_cap = 0;
+    uint32_t *d_park_ctl = nullptr;  // [0] parked count, [1] phase-2 cursor, [2] pixel cursor
+    U128 *d_seeds = nullptr;         // per-pixel RNG children of the current shard
+    uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
+    size_t diag_bytes = 0, diag_n = 0;
+    int n_cu = 0;
     uint32_t n_sph = 0, n_mats = 0;
     bool scene_set = false;
     // BVH (rtw_accel.h); has_bvh = false -> the filtered scan
     float4 *d_nodes = nullptr, *d_leaves = nullptr;
     uint32_t *d_always = nullptr;
-    uint32_t n_inner = 0, n_leaf = 0, n_always = 0;
+    uint32_t n_node = 0, n_leaf = 0, n_always = 0;
     bool has_bvh = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t last_stream = nullptr;
@@ -630,6 +992,7 @@ void upload_jump(rtw_session *s) {
 void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
     if ((n && !sp) || (nm && !m)) throw rtw::Error(RTW_E_ARG, "null scene buffer");
     if (nm > 65536) throw rtw::Error(RTW_E_UNSUPPORTED, "more than 65536 materials");
+    if (n > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "more than 65535 spheres (u16 path stack)");
     for (uint32_t i = 0; i < nm; ++i) {
         if (m[i].kind > RTW_DIELECTRIC) throw rtw::Error(RTW_E_ARG, "unknown material kind");
         if (m[i].kind == RTW_METAL && !(m[i].fuzz <= 1.))
@@ -643,19 +1006,18 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
     dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    dev_free(s->d_shade);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     s->d_sph = nullptr, s->d_filt = nullptr;
-    s->d_rad = nullptr, s->d_smat = nullptr, s->d_mats = nullptr;
+    s->d_shade = nullptr;
     s->d_nodes = nullptr, s->d_leaves = nullptr, s->d_always = nullptr;
     s->has_bvh = false, s->scene_set = false;
-    s->n_inner = s->n_leaf = s->n_always = 0;
+    s->n_node = s->n_leaf = s->n_always = 0;
     const uint32_t npad = (n + kChunk - 1) / kChunk * kChunk;
     std::vector<double4> a(n ? n : 1);
     // padding records can never be candidates (R2' = -inf -> disc = -inf)
     std::vector<float4> f(npad ? npad : kChunk, make_float4(0.f, 0.f, 0.f, -INFINITY));
-    std::vector<double> r(n ? n : 1);
-    std::vector<uint32_t> mi(n ? n : 1);
+    std::vector<ShadeRec> sh(n ? n : 1);
     for (uint32_t i = 0; i < n; ++i) {
         const double rad = sp[i].radius;
         const double rr = rad * rad;  // sphere.rs:49 `self.radius * self.radius`
@@ -666,19 +1028,20 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         const float r2p = rtw_accel::filter_r2p(c, rr);
         f[i] = make_float4(static_cast<float>(c[0]), static_cast<float>(c[1]),
                            static_cast<float>(c[2]), r2p);
-        r[i] = rad;
-        mi[i] = sp[i].mat;
+        // the sphere's material row, flattened next to its radius
+        const rtw_material &M = m[sp[i].mat];
+        ShadeRec &R = sh[i];
+        R.r = rad;
+        R.a0 = M.albedo[0], R.a1 = M.albedo[1], R.a2 = M.albedo[2];
+        R.p = M.kind == RTW_METAL ? M.fuzz : M.kind == RTW_DIELECTRIC ? M.ir : 0.;
+        R.kind = M.kind, R._pad = 0;
     }
     HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
     HIPCHECK(hipMalloc(&s->d_filt, f.size() * sizeof(float4)));
-    HIPCHECK(hipMalloc(&s->d_rad, r.size() * sizeof(double)));
-    HIPCHECK(hipMalloc(&s->d_smat, mi.size() * sizeof(uint32_t)));
-    HIPCHECK(hipMalloc(&s->d_mats, (nm ? nm : 1) * sizeof(rtw_material)));
+    HIPCHECK(hipMalloc(&s->d_shade, sh.size() * sizeof(ShadeRec)));
     HIPCHECK(hipMemcpy(s->d_sph, a.data(), a.size() * sizeof(double4), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(s->d_filt, f.data(), f.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_rad, r.data(), r.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_smat, mi.data(), mi.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    if (nm) HIPCHECK(hipMemcpy(s->d_mats, m, nm * sizeof(rtw_material), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(s->d_shade, sh.data(), sh.size() * sizeof(ShadeRec), hipMemcpyHostToDevice));
     // BVH over the same records (rtw_accel_build.cpp); ineligible scenes scan
     {
         std::vector<double> cen(3 * static_cast<size_t>(n)), rad(n);
@@ -699,7 +1062,7 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
             if (!bvh.always.empty())
                 HIPCHECK(hipMemcpy(s->d_always, bvh.always.data(), bvh.always.size() * sizeof(uint32_t),
                                    hipMemcpyHostToDevice));
-            s->n_inner = bvh.n_inner, s->n_leaf = bvh.n_leaf;
+            s->n_node = bvh.n_node, s->n_leaf = bvh.n_leaf;
             s->n_always = static_cast<uint32_t>(bvh.always.size());
             s->has_bvh = true;
         }
@@ -767,7 +1130,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.row_step = sh.row_step;
     P.n_rows = sh.n_rows;
     P.n_sph = s->n_sph;
-    P.n_inner = s->n_inner;
+    P.n_node = s->n_node;
     P.n_leaf = s->n_leaf;
     P.n_always = s->n_always;
     P.nodes = s->d_nodes;
@@ -778,9 +1141,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.seed_hi = seed.hi;
     P.sph = s->d_sph;
     P.filt = s->d_filt;
-    P.radius = s->d_rad;
-    P.sph_mat = s->d_smat;
-    P.mats = s->d_mats;
+    P.shade = s->d_shade;
     P.jump = s->d_jump;
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
@@ -797,6 +1158,32 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         s->spill_bytes = spill_need;
     }
     P.spill = s->d_spill;
+    // park queue (one slot per pixel) and the per-pixel segment budget of phase 1
+    const size_t npix_sh = static_cast<size_t>(sh.n_rows) * cam->img_width;
+    if (npix_sh > s->park_cap) {
+        HIPCHECK(hipSetDevice(s->device));
+        HIPCHECK(hipStreamSynchronize(stream ? stream : nullptr));
+        if (s->pending) HIPCHECK(hipEventSynchronize(s->ev1));
+        dev_free(s->d_park);
+        s->d_park = nullptr, s->park_cap = 0;
+        dev_free(s->d_seeds);
+        s->d_seeds = nullptr;
+        HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
+        HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
+        s->park_cap = npix_sh;
+    }
+    P.park = s->d_park;
+    P.park_count = s->d_park_ctl;
+    P.park_cursor = s->d_park_ctl + 1;
+    P.pix_cursor = s->d_park_ctl + 2;
+    P.seeds = s->d_seeds;
+    {
+        // budget = X x samples per pixel (X: RTW_BUDGET_X, default kBudgetX; 0 = off)
+        double bx = kBudgetX;
+        if (const char *e = std::getenv("RTW_BUDGET_X")) bx = std::atof(e);
+        const double b = bx * static_cast<double>(P.n_off);
+        P.seg_budget = (bx > 0. && b < 4e9) ? static_cast<uint32_t>(std::ceil(b)) : 0xffffffffu;
+    }
 #ifdef RTW_STAMPS
     {
         const size_t nw = static_cast<size_t>((P.W + kTile - 1) / kTile) * ((sh.n_rows + kTile - 1) / kTile) * 4;
@@ -814,6 +1201,23 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
 #endif
     P.counters = s->d_counters;
+    P.diag = nullptr;
+    if (const char *e = std::getenv("RTW_DIAG")) {
+        if (std::atoi(e) != 0) {
+            const size_t need = static_cast<size_t>(sh.n_rows) * cam->img_width * 2 * sizeof(uint32_t);
+            if (need > s->diag_bytes) {
+                HIPCHECK(hipSetDevice(s->device));
+                HIPCHECK(hipDeviceSynchronize());
+                dev_free(s->d_diag);
+                s->d_diag = nullptr, s->diag_bytes = 0;
+                HIPCHECK(hipMalloc(&s->d_diag, need));
+                s->diag_bytes = need;
+            }
+            HIPCHECK(hipMemsetAsync(s->d_diag, 0, need, stream));
+            P.diag = s->d_diag;
+            s->diag_n = need / sizeof(uint32_t);
+        }
+    }
 
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
@@ -824,13 +1228,44 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     if (const char *e = std::getenv("RTW_ACCEL")) mode = std::atoi(e);
     if (mode == kBvh && !s->has_bvh) mode = kScanF32;
     if (mode < kScanF64 || mode > kBvh) mode = kScanF32;
-    size_t lds = static_cast<size_t>(P.n_sph) * sizeof(double4);
-    if (mode == kBvh) lds += (static_cast<size_t>(P.n_inner) + P.n_leaf) * 2 * sizeof(float4);
+    size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh);
     const bool use_lds = lds <= kLdsCap;
     if (!use_lds) lds = 0;
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 4 * sizeof(uint32_t), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
-    if (P.n_rows) {
+    // phase 1: persistent per-lane refill (default) or one tile per workgroup (RTW_PERSIST=0)
+    bool persist = true;
+    if (const char *e = std::getenv("RTW_PERSIST")) persist = std::atoi(e) != 0;
+    P.order = 1;
+    if (const char *e = std::getenv("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
+    uint32_t grid_p = 0;
+    if (P.n_rows && persist) {
+        const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+        hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((npix + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, P);
+        HIPCHECK(hipGetLastError());
+        int pblock = kPBlock;
+        if (const char *e = std::getenv("RTW_PBLOCK")) pblock = std::atoi(e) == 1024 ? 1024 : kPBlock;
+        const void *fn = nullptr;
+#define RTW_PFN(L, M, T) reinterpret_cast<const void *>(&rtw_render_persist<L, M, T>)
+        if (pblock == 1024) {
+            if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(true, kScanF32, 1024) : RTW_PFN(true, kScanF64, 1024);
+            else fn = mode == kBvh ? RTW_PFN(false, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(false, kScanF32, 1024) : RTW_PFN(false, kScanF64, 1024);
+        } else {
+            if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(true, kScanF32, kPBlock) : RTW_PFN(true, kScanF64, kPBlock);
+            else fn = mode == kBvh ? RTW_PFN(false, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(false, kScanF32, kPBlock) : RTW_PFN(false, kScanF64, kPBlock);
+        }
+#undef RTW_PFN
+        int per_cu = 0;
+        HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, pblock, lds));
+        if (per_cu < 1) per_cu = 1;
+        grid_p = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(s->n_cu > 0 ? s->n_cu : 256);
+        const uint64_t need_blocks = (npix + pblock - 1) / pblock;
+        if (grid_p > need_blocks) grid_p = static_cast<uint32_t>(need_blocks);
+        void *args[] = {&P};
+        HIPCHECK(hipLaunchKernel(fn, dim3(grid_p), dim3(pblock), args, lds, st));
+    } else if (P.n_rows) {
 #define RTW_LAUNCH(L, M) hipLaunchKernelGGL((rtw_render_f64<L, M>), grid, dim3(kBlock), lds, st, P)
         if (use_lds) {
             if (mode == kBvh) RTW_LAUNCH(true, kBvh);
@@ -844,13 +1279,29 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
 #undef RTW_LAUNCH
         HIPCHECK(hipGetLastError());
     }
+    if (P.n_rows) {
+        if (P.seg_budget != 0xffffffffu) {  // phase 2: parked pixels, persistent coop groups
+            const size_t lds2 = lds_bytes_for(P.n_sph, 0, 0, false) + static_cast<size_t>(P.n_sph) * sizeof(float4);
+            const dim3 grid2(kCoopBlocks);
+            int g = 16;
+            if (const char *e = std::getenv("RTW_COOP")) g = std::atoi(e);
+            if (lds2 <= kLdsCap) {
+                if (g == 64) hipLaunchKernelGGL((rtw_finish_parked<true, 64>), grid2, dim3(kBlock), lds2, st, P);
+                else hipLaunchKernelGGL((rtw_finish_parked<true, 16>), grid2, dim3(kBlock), lds2, st, P);
+            } else {
+                if (g == 64) hipLaunchKernelGGL((rtw_finish_parked<false, 64>), grid2, dim3(kBlock), 0, st, P);
+                else hipLaunchKernelGGL((rtw_finish_parked<false, 16>), grid2, dim3(kBlock), 0, st, P);
+            }
+            HIPCHECK(hipGetLastError());
+        }
+    }
     HIPCHECK(hipEventRecord(s->ev1, st));
     s->last_stream = st;
     s->pending = true;
     s->last = rtw_stats{};
     s->last.pixels = static_cast<uint64_t>(P.n_rows) * P.W;
     s->last.samples = s->last.pixels * P.n_off;
-    s->last.grid_blocks = grid.x * grid.y;
+    s->last.grid_blocks = persist ? grid_p : grid.x * grid.y;
     s->last.block_threads = kBlock;
     s->last.accel = static_cast<uint32_t>(mode);
     s->last.lds_bytes = static_cast<uint32_t>(lds);
@@ -870,6 +1321,7 @@ void collect(rtw_session *s) {
     s->last.exact_wave_iterations = c[3];
     s->last.node_visits = c[4];
     s->last.brute_segments = c[5];
+    s->last.parked_pixels = c[6];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->pending = false;
@@ -892,6 +1344,8 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev0));
         HIPCHECK(hipEventCreate(&s->ev1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
+        HIPCHECK(hipMalloc(&s->d_park_ctl, 4 * sizeof(uint32_t)));
+        HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         upload_jump(s);
     } catch (...) {
         rtw_session_destroy(s);
@@ -937,9 +1391,10 @@ int rtw_session_destroy(rtw_session *s) {
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
     dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_rad), dev_free(s->d_smat), dev_free(s->d_mats);
+    dev_free(s->d_shade);
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
+    dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
@@ -971,6 +1426,17 @@ int rtw_session_stats(rtw_session *s, rtw_stats *out) {
     RTW_GUARD_BEGIN
     collect(s);
     *out = s->last;
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap) {
+    if (!s || (!out && cap)) return rtw::set_error("null argument"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    collect(s);
+    if (cap < s->diag_n) throw rtw::Error(RTW_E_CAPACITY, "diag buffer too small");
+    if (s->diag_n)
+        HIPCHECK(hipMemcpy(out, s->d_diag, s->diag_n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return RTW_OK;
     RTW_GUARD_END
 }

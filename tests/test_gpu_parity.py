@@ -167,12 +167,43 @@ def test_filter_stress_scenes():
         assert_same(fb, ref, st, seg)
 
 
-def test_filter_on_off_identical(monkeypatch):
-    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 90, 160, 50)
-    a, sa = gpu(cam, sph, n, mt, nm, 2, SEED)
-    monkeypatch.setenv("RTW_FILTER", "0")
-    b, sb = gpu(cam, sph, n, mt, nm, 2, SEED)
-    assert np.array_equal(a, b) and sa.segments == sb.segments
+STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x budget x group
+    ("0", "0", "16"), ("1", "0", "16"), ("2", "0", "16"),  # f64 scan / filtered scan / BVH
+    ("2", "0.01", "16"), ("2", "0.01", "64"),  # park every pixel after its first sample
+    ("2", "1.5", "16"), ("1", "2", "64"),      # park the heavier pixels
+    ("2", "1.5", "tile"), ("0", "0", "tile"),  # one-tile-per-workgroup phase 1 (RTW_PERSIST=0)
+]
+
+
+@pytest.mark.parametrize("accel,budget,coop", STRATEGIES)
+def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
+    """Every Scene::hit strategy and every phase-1 budget (including parking all
+    pixels into the cooperative kernel) gives the oracle's image bit-for-bit."""
+    monkeypatch.setenv("RTW_ACCEL", accel)
+    monkeypatch.setenv("RTW_BUDGET_X", budget)
+    monkeypatch.setenv("RTW_COOP", coop if coop != "tile" else "16")
+    monkeypatch.setenv("RTW_PERSIST", "0" if coop == "tile" else "1")
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
+    fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
+    ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
+    assert_same(fb, ref, st, seg)
+    assert st.accel == int(accel)
+    if budget == "0.01":
+        assert st.parked_pixels == 45 * 80
+    if budget == "0":
+        assert st.parked_pixels == 0
+    if accel == "2" and budget == "0":
+        assert st.node_visits > 0 and st.brute_segments < st.segments // 100
+
+
+@pytest.mark.parametrize("accel,budget,coop", [("2", "0.01", "16"), ("2", "0.7", "64")])
+def test_strategies_on_stress_and_deep_scenes(monkeypatch, tmp_path, accel, budget, coop):
+    monkeypatch.setenv("RTW_ACCEL", accel)
+    monkeypatch.setenv("RTW_BUDGET_X", budget)
+    monkeypatch.setenv("RTW_COOP", coop)
+    test_filter_stress_scenes()
+    test_deep_paths_use_spill_levels()
+    test_custom_scene_through_trait_surface(tmp_path)
 
 
 def test_shards_reassemble_bit_exact():

@@ -99,8 +99,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
     uint64_t c0 = 0, c1 = 0;
     uint32_t nc = 0, visits = 0;
     const bool ok = walk(reinterpret_cast<const F4 *>(S.bvh.nodes.data()),
-                         reinterpret_cast<const F4 *>(S.bvh.leaves.data()), S.bvh.n_inner, wr, U, c0,
-                         c1, nc, visits);
+                         reinterpret_cast<const F4 *>(S.bvh.leaves.data()), wr, U, c0, c1, nc, visits);
     k.visits += visits;
     if (visits > k.max_visits) k.max_visits = visits;
     k.cands += nc;
@@ -271,7 +270,7 @@ int main(int argc, char **argv) {
            "\"rays\": %llu, \"hits\": %llu, \"walked\": %llu, \"visits_per_walk\": %.3f, \"max_visits\": %llu, "
            "\"cands_per_walk\": %.3f, \"fallbacks\": %llu, \"overflows\": %llu, \"not_walkable\": %llu, "
            "\"mismatches\": %llu}\n",
-           name.c_str(), S.n, S.bvh.always.size(), S.bvh.n_inner, S.bvh.depth, (unsigned long long)k.rays,
+           name.c_str(), S.n, S.bvh.always.size(), S.bvh.n_node, S.bvh.depth, (unsigned long long)k.rays,
            (unsigned long long)k.hits, (unsigned long long)k.walked,
            k.walked ? double(k.visits) / k.walked : 0., (unsigned long long)k.max_visits,
            k.walked ? double(k.cands) / k.walked : 0., (unsigned long long)k.fallbacks,
