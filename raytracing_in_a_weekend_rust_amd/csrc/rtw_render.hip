@@ -47,8 +47,9 @@ constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
-constexpr int kCounters = 7;
-constexpr double kBudgetX = 6.0;        // phase-1 segment budget per pixel, x samples per pixel
+constexpr int kCounters = 8;
+constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
+constexpr uint32_t kHeavyPerBlock = 1;  // priority waves per persistent workgroup (parked pixels)
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 
 // Scene::hit strategies (one kernel instantiation each)
@@ -98,7 +99,9 @@ struct KParams {
     uint32_t row_begin, row_step, n_rows, n_sph;
     uint32_t jump_bits, _pad;
     uint32_t n_node, n_leaf, n_always, seg_budget;
-    uint32_t order, _pad3;
+    uint32_t order, heavy_per_block;
+    uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
+    uint32_t n_cursor_waves, _pad4;
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -116,9 +119,11 @@ struct KParams {
     U128 *seeds;                // per-pixel RNG children (persistent phase 1)
     uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
+    uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
+    uint32_t *park_flag;        // per park slot: 1 once the entry is published
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
                                    // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
-                                   // [6] parked pixels
+                                   // [6] parked pixels, [7] queue spin timeouts
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -728,6 +733,36 @@ __global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
 // shard from a global cursor (one atomic per wave per refill). Waves stay full
 // until the cursor runs dry, so the launch ends within about one pixel's
 // duration of the last pixel handed out.
+// Shared words of the park queue (agent scope): relaxed atomics; payload stored
+// write-through (sc1) by 8-byte atomic stores, then a drain, then the flag
+// (cdna_hip_programming.md Guideline 16, recipe R1); consumers poll the flag
+// relaxed and take ONE agent-scope acquire before plain loads.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
+    return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_parked(const KParams &P, const Parked &q) {
+    const uint32_t slot = atomicAdd(P.park_count, 1u);
+    const unsigned long long *w = reinterpret_cast<const unsigned long long *>(&q);
+    gu64 *dst = (gu64 *)(P.park + slot);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) __hip_atomic_store(dst + j, w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store((gu32 *)(P.park_flag + slot), 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Phase 1, persistent form: every lane runs one pixel at a time and, when the
+// pixel completes, takes the next pixel of the shard from a global cursor (one
+// atomic per wave per refill). A pixel whose cost runs away -- more than
+// P.rate_x segments per sample after P.rate_k samples, or P.seg_budget segments
+// in all -- parks at a sample boundary in the park queue. The first
+// P.heavy_per_block waves of every workgroup run at raised issue priority and
+// take only parked pixels, so the heaviest pixels' serial chains run at close to
+// a lone wave's latency while the other waves keep the chip busy; waves whose
+// cursor ran dry also drain the queue. Every wave exits once every cursor-taking
+// wave has signalled that it will park no more and the queue is empty.
 template <bool kLds, int kMode, int kThreads>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
@@ -738,6 +773,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
     const uint64_t stride = npix;
+    const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
+    if (heavy_wave) __builtin_amdgcn_s_setprio(3);
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
@@ -747,44 +784,113 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
         }
     };
-    bool need = true;
+    bool need = true;        // lane holds no pixel
+    bool from_cursor = false;  // lane's pixel came from the cursor (may park)
+    bool cursor_dry = heavy_wave;  // wave-uniform: no more cursor pixels for this wave
+    bool signaled = heavy_wave;    // wave-uniform: told P.park_ctl[3] it parks no more
     uint32_t x = 0, lr = 0, pseg = 0;
     uint64_t pix = 0;
     PixelState ps;
     Path p;
     PixelLoc pl;
+    uint32_t idle_rounds = 0;
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    auto start_pixel = [&]() -> bool {  // false: pixel needs no segment (written already)
+        pix = static_cast<uint64_t>(lr) * P.W + x;
+        pseg = 0;
+        if (P.max_depth == 0 || ps.k >= P.n_off) {  // every sample black, no Scene::hit call
+            ps.k = P.n_off;
+            write_pixel(P, x, lr, ps);
+            return false;
+        }
+        pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
+        gen_ray(P, pl, ps.k, ps.rng, p);
+        return true;
+    };
     for (;;) {
         {  // the wave's first active lane counts the wave-level iteration
             const uint64_t exm = __builtin_amdgcn_read_exec();
             tl.witer += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
         }
-        if (need) {  // refill: one atomic for all lanes of the wave that need a pixel
+        bool dry_now = false;
+        if (need && !cursor_dry) {  // cursor refill: one atomic for the wave's idle lanes
             const uint64_t m = __ballot(1);
             const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
             uint32_t base = 0;
             if (rank == 0) base = atomicAdd(P.pix_cursor, static_cast<uint32_t>(__popcll(m)));
             base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
             const uint64_t ticket = static_cast<uint64_t>(base) + rank;
-            if (ticket >= npix) break;
-            // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
-            // cheapest in the book's scenes, go last and fill the drain)
-            const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
-            x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
-            lr = P.order ? P.n_rows - 1u - tr : tr;
-            pix = static_cast<uint64_t>(lr) * P.W + x;
-            ps.rng = P.seeds[pix];
-            ps.k = 0;
-            ps.ar = ps.ag = ps.ab = 0.;
-            pseg = 0;
-            if (P.max_depth == 0) {  // every sample black, no Scene::hit call
-                ps.k = P.n_off;
-                write_pixel(P, x, lr, ps);
-                continue;
+            if (ticket < npix) {
+                // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
+                // cheapest in the book's scenes, go last and fill the drain)
+                const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
+                x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
+                lr = P.order ? P.n_rows - 1u - tr : tr;
+                ps.rng = P.seeds[static_cast<uint64_t>(lr) * P.W + x];
+                ps.k = 0;
+                ps.ar = ps.ag = ps.ab = 0.;
+                from_cursor = true;
+                need = !start_pixel();
+            } else {
+                dry_now = true;
             }
-            pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
-            gen_ray(P, pl, 0, ps.rng, p);
-            need = false;
         }
+        cursor_dry = cursor_dry || __any(dry_now);  // wave-uniform
+        if (cursor_dry && !signaled && __ballot(!need && from_cursor) == 0) {
+            // no cursor pixel left in this wave: it parks no more
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1))
+                atomicAdd(P.park_ctl_done, 1u);
+            signaled = true;
+        }
+        if (need && cursor_dry) {  // queue refill (parked pixels), heavy waves first
+            const uint64_t m = __ballot(1);
+            const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+            const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
+            uint32_t base = 0, take = 0;
+            if (rank == 0) {
+                const uint32_t c = ld_rlx(P.park_cursor), n = ld_rlx(P.park_count);
+                if (n > c) {
+                    take = min(static_cast<uint32_t>(__popcll(m)), n - c);
+                    if (atomicCAS(P.park_cursor, c, c + take) != c) take = 0;
+                    base = c;
+                }
+            }
+            base = __shfl(base, leader), take = __shfl(take, leader);
+            if (rank < take) {
+                const uint32_t t = base + rank;
+                uint32_t spins = 0;
+                while (ld_rlx(P.park_flag + t) != 1u) {  // the producer has reserved t: soon
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1u << 24)) break;
+                }
+                if (spins > (1u << 24)) {
+                    atomicAdd(&P.counters[7], 1ull);
+                } else {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const Parked q = P.park[t];
+                    x = q.x, lr = q.lr;
+                    ps.rng = U128{q.rng_lo, q.rng_hi};
+                    ps.k = q.k;
+                    ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
+                    from_cursor = false;
+                    need = !start_pixel();
+                }
+            }
+        }
+        if (__all(need)) {  // wave idle: done, or wait for parked pixels
+            if (cursor_dry && ld_rlx(P.park_ctl_done) >= P.n_cursor_waves &&
+                ld_rlx(P.park_cursor) >= ld_rlx(P.park_count))
+                break;
+            __builtin_amdgcn_s_sleep(8);
+            if (++idle_rounds > (1u << 20) &&
+                __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
+                atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
+                break;
+            }
+            continue;
+        }
+        if (need) continue;  // this lane waits while the others work
         ++tl.seg, ++pseg;
         const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
         double bt = 0.;
@@ -793,20 +899,21 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, cr, cg, cb)) {
             fold(P, sv.shd, p, pix, stride, cr, cg, cb, ps);
             const bool done = ++ps.k >= P.n_off;
-            if ((done || pseg >= P.seg_budget) && P.diag) {
-                P.diag[2 * pix] = pseg;
+            const bool park = !done && from_cursor &&
+                              (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
+            if ((done || park) && P.diag) {
+                P.diag[2 * pix] += pseg;
                 P.diag[2 * pix + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
             }
             if (done) {
                 write_pixel(P, x, lr, ps);
                 need = true;
-            } else if (pseg >= P.seg_budget) {  // park at the sample boundary
-                const uint32_t slot = atomicAdd(P.park_count, 1u);
+            } else if (park) {  // park at the sample boundary
                 Parked q;
                 q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
                 q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
                 q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
-                P.park[slot] = q;
+                publish_parked(P, q);
                 ++tl.parked;
                 need = true;
             } else {
@@ -955,6 +1062,7 @@ struct rtw_session {
     size_t park_cap = 0;
     uint32_t *d_park_ctl = nullptr;  // [0] parked count, [1] phase-2 cursor, [2] pixel cursor
     U128 *d_seeds = nullptr;         // per-pixel RNG children of the current shard
+    uint32_t *d_park_flag = nullptr; // per park slot publish flags
     uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
     size_t diag_bytes = 0, diag_n = 0;
     int n_cu = 0;
@@ -1166,16 +1274,19 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (s->pending) HIPCHECK(hipEventSynchronize(s->ev1));
         dev_free(s->d_park);
         s->d_park = nullptr, s->park_cap = 0;
-        dev_free(s->d_seeds);
-        s->d_seeds = nullptr;
+        dev_free(s->d_seeds), dev_free(s->d_park_flag);
+        s->d_seeds = nullptr, s->d_park_flag = nullptr;
         HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
         HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
+        HIPCHECK(hipMalloc(&s->d_park_flag, npix_sh * sizeof(uint32_t)));
         s->park_cap = npix_sh;
     }
     P.park = s->d_park;
     P.park_count = s->d_park_ctl;
     P.park_cursor = s->d_park_ctl + 1;
     P.pix_cursor = s->d_park_ctl + 2;
+    P.park_ctl_done = s->d_park_ctl + 3;
+    P.park_flag = s->d_park_flag;
     P.seeds = s->d_seeds;
     {
         // budget = X x samples per pixel (X: RTW_BUDGET_X, default kBudgetX; 0 = off)
@@ -1263,6 +1374,18 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         grid_p = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(s->n_cu > 0 ? s->n_cu : 256);
         const uint64_t need_blocks = (npix + pblock - 1) / pblock;
         if (grid_p > need_blocks) grid_p = static_cast<uint32_t>(need_blocks);
+        // heavy waves per workgroup (RTW_HEAVY, default 1): raised priority, parked pixels only
+        uint32_t heavy = kHeavyPerBlock;
+        if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
+        const uint32_t wpb = static_cast<uint32_t>(pblock) / 64u;
+        if (heavy >= wpb) heavy = wpb - 1;
+        P.heavy_per_block = heavy;
+        P.n_cursor_waves = grid_p * (wpb - heavy);
+        P.rate_k = 16, P.rate_x = 8;
+        if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
+        if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
+        HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};
         HIPCHECK(hipLaunchKernel(fn, dim3(grid_p), dim3(pblock), args, lds, st));
     } else if (P.n_rows) {
@@ -1279,8 +1402,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
 #undef RTW_LAUNCH
         HIPCHECK(hipGetLastError());
     }
-    if (P.n_rows) {
-        if (P.seg_budget != 0xffffffffu) {  // phase 2: parked pixels, persistent coop groups
+    if (P.n_rows && !persist) {
+        if (P.seg_budget != 0xffffffffu) {  // phase 2 of the tile kernel: parked pixels, coop groups
             const size_t lds2 = lds_bytes_for(P.n_sph, 0, 0, false) + static_cast<size_t>(P.n_sph) * sizeof(float4);
             const dim3 grid2(kCoopBlocks);
             int g = 16;
@@ -1395,6 +1518,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
+    dev_free(s->d_park_flag);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);

@@ -172,6 +172,8 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0.01", "16"), ("2", "0.01", "64"),  # park every pixel after its first sample
     ("2", "1.5", "16"), ("1", "2", "64"),      # park the heavier pixels
     ("2", "1.5", "tile"), ("0", "0", "tile"),  # one-tile-per-workgroup phase 1 (RTW_PERSIST=0)
+    ("2", "0.3", "heavy0"), ("2", "2", "heavy3"),  # persistent: drain by plain waves / 3 priority waves
+    ("2", "0", "rate1"),                        # rate-based parking of nearly every pixel
 ]
 
 
@@ -181,8 +183,11 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     pixels into the cooperative kernel) gives the oracle's image bit-for-bit."""
     monkeypatch.setenv("RTW_ACCEL", accel)
     monkeypatch.setenv("RTW_BUDGET_X", budget)
-    monkeypatch.setenv("RTW_COOP", coop if coop != "tile" else "16")
+    monkeypatch.setenv("RTW_COOP", coop if coop in ("16", "64") else "16")
     monkeypatch.setenv("RTW_PERSIST", "0" if coop == "tile" else "1")
+    monkeypatch.setenv("RTW_HEAVY", {"heavy0": "0", "heavy3": "3"}.get(coop, "1"))
+    monkeypatch.setenv("RTW_RATE_X", "1" if coop == "rate1" else "8")
+    monkeypatch.setenv("RTW_RATE_K", "2" if coop == "rate1" else "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
     fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
     ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
@@ -190,8 +195,10 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     assert st.accel == int(accel)
     if budget == "0.01":
         assert st.parked_pixels == 45 * 80
-    if budget == "0":
+    if budget == "0" and coop != "rate1":
         assert st.parked_pixels == 0
+    if coop == "rate1":
+        assert st.parked_pixels > 45 * 80 // 2
     if accel == "2" and budget == "0":
         assert st.node_visits > 0 and st.brute_segments < st.segments // 100
 
