@@ -84,6 +84,12 @@ struct U128 {
     uint64_t lo, hi;
 };
 
+// Global words shared across workgroups (and so across XCDs, whose L2s are not
+// coherent with each other) are accessed as agent-scope atomics: sc1 loads and
+// write-through stores.
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
 // Per-sphere shading record (48 B): the sphere's radius and its material row
 // flattened (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric).
 struct ShadeRec {
@@ -111,7 +117,7 @@ struct KParams {
     const ShadeRec *shade;      // per-sphere radius + material
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
-    uint16_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
+    uint32_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
     struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
     uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
@@ -121,6 +127,7 @@ struct KParams {
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
     uint32_t *park_flag;        // per park slot: 1 once the entry is published
+    uint32_t *pixels_done;      // pixels written (completeness check of the persistent kernel)
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
                                    // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
                                    // [6] parked pixels, [7] queue spin timeouts
@@ -211,20 +218,27 @@ __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &u
 // (one u16 per pixel per level). No private/scratch memory is used: a scratch
 // array caps the waves a CU may hold.
 constexpr uint32_t kRegSlots = 8;
+// A pixel can move between workgroups (parking), so its spill entries can be
+// written on one XCD and later on another: they are write-through stores and
+// sc1 loads, never dirty L2 lines that a late write-back could replay over the
+// newer owner's entries.
 struct PathStack {
     uint64_t r0 = 0, r1 = 0;
     uint32_t n = 0;
-    __device__ __forceinline__ void push(uint32_t v, uint16_t *spill, uint64_t stride, uint64_t pix) {
+    __device__ __forceinline__ void push(uint32_t v, uint32_t *spill, uint64_t stride, uint64_t pix) {
         if (n < 4) r0 |= static_cast<uint64_t>(v) << (16u * n);
         else if (n < kRegSlots) r1 |= static_cast<uint64_t>(v) << (16u * (n - 4u));
-        else spill[static_cast<uint64_t>(n - kRegSlots) * stride + pix] = static_cast<uint16_t>(v);
+        else
+            __hip_atomic_store((gu32 *)(spill + static_cast<uint64_t>(n - kRegSlots) * stride + pix), v,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ++n;
     }
-    __device__ __forceinline__ uint32_t at(uint32_t j, const uint16_t *spill, uint64_t stride,
+    __device__ __forceinline__ uint32_t at(uint32_t j, uint32_t *spill, uint64_t stride,
                                            uint64_t pix) const {
         if (j < 4) return static_cast<uint32_t>(r0 >> (16u * j)) & 0xffffu;
         if (j < kRegSlots) return static_cast<uint32_t>(r1 >> (16u * (j - 4u))) & 0xffffu;
-        return spill[static_cast<uint64_t>(j - kRegSlots) * stride + pix];
+        return __hip_atomic_load((gu32 *)(spill + static_cast<uint64_t>(j - kRegSlots) * stride + pix),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __device__ __forceinline__ void clear() { r0 = r1 = 0, n = 0; }
 };
@@ -467,6 +481,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
 
 __device__ __forceinline__ void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
                                             const PixelState &ps) {
+    if (P.pixels_done) atomicAdd(P.pixels_done, 1u);
     const double nf = static_cast<double>(P.n_off);
     double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
     o[0] = ps.ar / nf;
@@ -728,17 +743,10 @@ __global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
                                      P.jump, P.jump_bits));
 }
 
-// Phase 1, persistent form: every lane runs one pixel at a time and, when the
-// pixel completes (or parks at the segment budget), takes the next pixel of the
-// shard from a global cursor (one atomic per wave per refill). Waves stay full
-// until the cursor runs dry, so the launch ends within about one pixel's
-// duration of the last pixel handed out.
 // Shared words of the park queue (agent scope): relaxed atomics; payload stored
 // write-through (sc1) by 8-byte atomic stores, then a drain, then the flag
 // (cdna_hip_programming.md Guideline 16, recipe R1); consumers poll the flag
-// relaxed and take ONE agent-scope acquire before plain loads.
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
+// relaxed and load the entry by sc1 loads (no stale copy of a reused slot).
 __device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
     return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -751,177 +759,6 @@ __device__ __forceinline__ void publish_parked(const KParams &P, const Parked &q
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store((gu32 *)(P.park_flag + slot), 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Phase 1, persistent form: every lane runs one pixel at a time and, when the
-// pixel completes, takes the next pixel of the shard from a global cursor (one
-// atomic per wave per refill). A pixel whose cost runs away -- more than
-// P.rate_x segments per sample after P.rate_k samples, or P.seg_budget segments
-// in all -- parks at a sample boundary in the park queue. The first
-// P.heavy_per_block waves of every workgroup run at raised issue priority and
-// take only parked pixels, so the heaviest pixels' serial chains run at close to
-// a lone wave's latency while the other waves keep the chip busy; waves whose
-// cursor ran dry also drain the queue. Every wave exits once every cursor-taking
-// wave has signalled that it will park no more and the queue is empty.
-template <bool kLds, int kMode, int kThreads>
-__global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
-    const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
-    const double4 *sph = sv.sph;
-    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
-    Tally tl;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
-    const uint64_t stride = npix;
-    const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
-    if (heavy_wave) __builtin_amdgcn_s_setprio(3);
-    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
-                   double &bt) -> int {
-        if constexpr (kMode == kBvh) {
-            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
-        } else {
-            const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
-            return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
-        }
-    };
-    bool need = true;        // lane holds no pixel
-    bool from_cursor = false;  // lane's pixel came from the cursor (may park)
-    bool cursor_dry = heavy_wave;  // wave-uniform: no more cursor pixels for this wave
-    bool signaled = heavy_wave;    // wave-uniform: told P.park_ctl[3] it parks no more
-    uint32_t x = 0, lr = 0, pseg = 0;
-    uint64_t pix = 0;
-    PixelState ps;
-    Path p;
-    PixelLoc pl;
-    uint32_t idle_rounds = 0;
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    auto start_pixel = [&]() -> bool {  // false: pixel needs no segment (written already)
-        pix = static_cast<uint64_t>(lr) * P.W + x;
-        pseg = 0;
-        if (P.max_depth == 0 || ps.k >= P.n_off) {  // every sample black, no Scene::hit call
-            ps.k = P.n_off;
-            write_pixel(P, x, lr, ps);
-            return false;
-        }
-        pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
-        gen_ray(P, pl, ps.k, ps.rng, p);
-        return true;
-    };
-    for (;;) {
-        {  // the wave's first active lane counts the wave-level iteration
-            const uint64_t exm = __builtin_amdgcn_read_exec();
-            tl.witer += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
-        }
-        bool dry_now = false;
-        if (need && !cursor_dry) {  // cursor refill: one atomic for the wave's idle lanes
-            const uint64_t m = __ballot(1);
-            const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
-            uint32_t base = 0;
-            if (rank == 0) base = atomicAdd(P.pix_cursor, static_cast<uint32_t>(__popcll(m)));
-            base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
-            const uint64_t ticket = static_cast<uint64_t>(base) + rank;
-            if (ticket < npix) {
-                // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
-                // cheapest in the book's scenes, go last and fill the drain)
-                const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
-                x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
-                lr = P.order ? P.n_rows - 1u - tr : tr;
-                ps.rng = P.seeds[static_cast<uint64_t>(lr) * P.W + x];
-                ps.k = 0;
-                ps.ar = ps.ag = ps.ab = 0.;
-                from_cursor = true;
-                need = !start_pixel();
-            } else {
-                dry_now = true;
-            }
-        }
-        cursor_dry = cursor_dry || __any(dry_now);  // wave-uniform
-        if (cursor_dry && !signaled && __ballot(!need && from_cursor) == 0) {
-            // no cursor pixel left in this wave: it parks no more
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1))
-                atomicAdd(P.park_ctl_done, 1u);
-            signaled = true;
-        }
-        if (need && cursor_dry) {  // queue refill (parked pixels), heavy waves first
-            const uint64_t m = __ballot(1);
-            const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
-            const int leader = __ffsll(static_cast<unsigned long long>(m)) - 1;
-            uint32_t base = 0, take = 0;
-            if (rank == 0) {
-                const uint32_t c = ld_rlx(P.park_cursor), n = ld_rlx(P.park_count);
-                if (n > c) {
-                    take = min(static_cast<uint32_t>(__popcll(m)), n - c);
-                    if (atomicCAS(P.park_cursor, c, c + take) != c) take = 0;
-                    base = c;
-                }
-            }
-            base = __shfl(base, leader), take = __shfl(take, leader);
-            if (rank < take) {
-                const uint32_t t = base + rank;
-                uint32_t spins = 0;
-                while (ld_rlx(P.park_flag + t) != 1u) {  // the producer has reserved t: soon
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (1u << 24)) break;
-                }
-                if (spins > (1u << 24)) {
-                    atomicAdd(&P.counters[7], 1ull);
-                } else {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    const Parked q = P.park[t];
-                    x = q.x, lr = q.lr;
-                    ps.rng = U128{q.rng_lo, q.rng_hi};
-                    ps.k = q.k;
-                    ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
-                    from_cursor = false;
-                    need = !start_pixel();
-                }
-            }
-        }
-        if (__all(need)) {  // wave idle: done, or wait for parked pixels
-            if (cursor_dry && ld_rlx(P.park_ctl_done) >= P.n_cursor_waves &&
-                ld_rlx(P.park_cursor) >= ld_rlx(P.park_count))
-                break;
-            __builtin_amdgcn_s_sleep(8);
-            if (++idle_rounds > (1u << 20) &&
-                __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
-                atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
-                break;
-            }
-            continue;
-        }
-        if (need) continue;  // this lane waits while the others work
-        ++tl.seg, ++pseg;
-        const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
-        double bt = 0.;
-        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
-        double cr, cg, cb;
-        if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, cr, cg, cb)) {
-            fold(P, sv.shd, p, pix, stride, cr, cg, cb, ps);
-            const bool done = ++ps.k >= P.n_off;
-            const bool park = !done && from_cursor &&
-                              (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
-            if ((done || park) && P.diag) {
-                P.diag[2 * pix] += pseg;
-                P.diag[2 * pix + 1] = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
-            }
-            if (done) {
-                write_pixel(P, x, lr, ps);
-                need = true;
-            } else if (park) {  // park at the sample boundary
-                Parked q;
-                q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
-                q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
-                q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
-                publish_parked(P, q);
-                ++tl.parked;
-                need = true;
-            } else {
-                gen_ray(P, pl, ps.k, ps.rng, p);
-            }
-        }
-    }
-    flush_tally(P, tl, false);
 }
 
 // (t, index) minimum across a group of `kG` lanes (16 or 64): DPP butterflies
@@ -956,19 +793,246 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
 // LDS-staged pass-1 records, runs the exact f64 test on its candidates, then
 // the group takes the (t, index) minimum. Every lane of a group then runs the
 // identical scatter on the identical RNG state.
+// One parked pixel finished by a group of kG lanes (all lanes of the group run
+// the identical path; lane j of the group filters spheres j, j + kG, ...).
+// Returns the pixel's segments on the group's first lane (0 on the others).
+template <uint32_t kG>
+__device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
+                                               const float4 *__restrict__ filt, const Parked &q,
+                                               Tally &tl) {
+    const uint32_t sub = threadIdx.x & (kG - 1u);
+    const uint32_t n = P.n_sph;
+    const double4 *sph = sv.sph;
+    const uint32_t y = P.row_begin + q.lr * P.row_step;
+    PixelState ps;
+    ps.rng = U128{q.rng_lo, q.rng_hi};
+    ps.k = q.k;
+    ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
+    const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
+    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                   double &bt) -> int {
+        const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
+        int best = -1;
+        bt = 0.;
+        for (uint32_t base = 0; base < n; base += 32u * kG) {
+            uint32_t mask = 0;  // bit j: sphere base + sub + j*kG is a candidate
+#pragma unroll 8
+            for (uint32_t j = 0; j < 32u; ++j) {
+                const uint32_t i = base + sub + j * kG;
+                if (i < n && (!g.fast || g.pass(filt[i]))) mask |= 1u << j;
+            }
+            while (mask) {
+                const uint32_t j = static_cast<uint32_t>(__builtin_ctz(mask));
+                mask &= mask - 1u;
+                ++tl.ntest;
+                exact_test(sph, base + sub + j * kG, ox, oy, oz, dx, dy, dz, a, best, bt);
+            }
+        }
+        group_min<kG>(bt, best);
+        return best;
+    };
+    uint32_t s = 0;
+    Stamps stp;
+    trace_samples(P, sv, q.x, y, pix, ps, 0xffffffffu, s, stp, hit);
+    if (sub == 0) {
+        write_pixel(P, q.x, q.lr, ps);
+        if (P.diag) {
+            atomicAdd(P.diag + 2 * pix, s);
+            __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
+                               static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return s;
+    }
+    return 0;
+}
+
+// pass-1 records staged in LDS after the scene view (cooperative groups scan them)
+template <bool kLds>
+__device__ __forceinline__ const float4 *stage_filt(const KParams &P, float4 *lf) {
+    if (!kLds) return P.filt;
+    for (uint32_t i = threadIdx.x; i < P.n_sph; i += blockDim.x) lf[i] = P.filt[i];
+    __syncthreads();
+    return lf;
+}
+
+// Phase 1, persistent form, with the heavy tail folded in. Every lane of a
+// cursor wave runs one pixel at a time and, when the pixel completes, takes the
+// next pixel of the shard from a global cursor (one atomic per wave per refill).
+// A pixel whose cost runs away -- more than P.rate_x segments per sample after
+// P.rate_k samples, or P.seg_budget segments in all -- parks at a sample
+// boundary in the park queue (published write-through, Guideline 16 R1). Parked
+// pixels are finished by 16-lane cooperative groups (coop_pixel): from the start
+// by the first P.heavy_per_block waves of every workgroup, which run at raised
+// issue priority and do nothing else, and at the end by every cursor wave whose
+// cursor ran dry. Groups claim queue tickets in order and wait for a claimed
+// ticket to be published; they stop once every cursor wave has signalled that it
+// parks no more and their ticket lies past the final queue length.
+constexpr uint32_t kCoopG = 16;
+template <bool kLds, int kMode, int kThreads>
+__global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
+    // pass-1 records after the scene view: after the leaves (BVH) or the shading records
+    float4 *filt_lds = reinterpret_cast<float4 *>(reinterpret_cast<ShadeRec *>(lds_sph + P.n_sph) + P.n_sph);
+    if (kMode == kBvh) filt_lds += 8u * P.n_node + 2u * P.n_leaf;
+    const float4 *filt = stage_filt<kLds>(P, filt_lds);
+    const double4 *sph = sv.sph;
+    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
+    Tally tl;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+    const uint64_t stride = npix;
+    const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
+    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                   double &bt) -> int {
+        if constexpr (kMode == kBvh) {
+            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
+        } else {
+            const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
+            return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
+        }
+    };
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (heavy_wave) {
+        __builtin_amdgcn_s_setprio(3);
+    } else {
+        bool need = true;  // lane holds no pixel
+        bool dry = false;  // wave-uniform: the cursor ran dry
+        uint32_t x = 0, lr = 0, pseg = 0;
+        uint64_t pix = 0;
+        PixelState ps;
+        Path p;
+        PixelLoc pl;
+        for (;;) {
+            {  // the wave's first active lane counts the wave-level iteration
+                const uint64_t exm = __builtin_amdgcn_read_exec();
+                tl.witer += static_cast<uint32_t>(__builtin_ctzll(exm) == static_cast<int>(lane));
+            }
+            bool dry_now = false;
+            if (need && !dry) {  // refill: one atomic for the wave's idle lanes
+                const uint64_t m = __ballot(1);
+                const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+                uint32_t base = 0;
+                if (rank == 0) base = atomicAdd(P.pix_cursor, static_cast<uint32_t>(__popcll(m)));
+                base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
+                const uint64_t ticket = static_cast<uint64_t>(base) + rank;
+                if (ticket < npix) {
+                    // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
+                    // cheapest in the book's scenes, go last and fill the drain)
+                    const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
+                    x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
+                    lr = P.order ? P.n_rows - 1u - tr : tr;
+                    pix = static_cast<uint64_t>(lr) * P.W + x;
+                    ps.rng = P.seeds[pix];
+                    ps.k = 0;
+                    ps.ar = ps.ag = ps.ab = 0.;
+                    pseg = 0;
+                    if (P.max_depth == 0) {  // every sample black, no Scene::hit call
+                        ps.k = P.n_off;
+                        write_pixel(P, x, lr, ps);
+                    } else {
+                        pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
+                        gen_ray(P, pl, 0, ps.rng, p);
+                        need = false;
+                    }
+                } else {
+                    dry_now = true;
+                }
+            }
+            dry = dry || __any(dry_now);  // wave-uniform
+            if (__all(need)) {
+                if (dry) break;
+                continue;
+            }
+            if (need) continue;  // this lane waits while the others work
+            ++tl.seg, ++pseg;
+            const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+            double bt = 0.;
+            const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+            double cr, cg, cb;
+            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, cr, cg, cb)) {
+                fold(P, sv.shd, p, pix, stride, cr, cg, cb, ps);
+                const bool done = ++ps.k >= P.n_off;
+                const bool park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
+                if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
+                    atomicAdd(P.diag + 2 * pix, pseg);
+                    __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
+                                       static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                if (done) {
+                    write_pixel(P, x, lr, ps);
+                    need = true;
+                } else if (park) {  // park at the sample boundary
+                    Parked q;
+                    q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
+                    q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
+                    q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
+                    publish_parked(P, q);
+                    ++tl.parked;
+                    need = true;
+                } else {
+                    gen_ray(P, pl, ps.k, ps.rng, p);
+                }
+            }
+        }
+        // this wave parks no more (its parks are published: drained stores + flags)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1))
+            atomicAdd(P.park_ctl_done, 1u);
+    }
+    // cooperative drain of the park queue, kCoopG lanes per parked pixel
+    const uint32_t sub = threadIdx.x & (kCoopG - 1u);
+    const int gl = static_cast<int>(lane & ~(kCoopG - 1u));
+    uint32_t cseg = 0;
+    for (;;) {
+        uint32_t t = 0, state = 0;  // state 1: ticket t is published, 2: stop
+        if (sub == 0) {
+            t = atomicAdd(P.park_cursor, 1u);
+            for (uint32_t spins = 0;; ++spins) {
+                if (t < ld_rlx(P.park_count)) {
+                    while (ld_rlx(P.park_flag + t) != 1u) __builtin_amdgcn_s_sleep(2);
+                    state = 1;
+                    break;
+                }
+                const uint32_t dn = ld_rlx(P.park_ctl_done);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (dn >= P.n_cursor_waves && t >= ld_rlx(P.park_count)) {
+                    state = 2;  // every cursor wave is done and t lies past the queue
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(16);
+                if ((spins & 1023u) == 1023u &&
+                    __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
+                    atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
+                    state = 2;
+                    break;
+                }
+            }
+        }
+        t = __shfl(t, gl);
+        state = __shfl(state, gl);
+        if (state == 2) break;
+        // every load of the handed-off entry is an sc1 load (Guideline 16)
+        Parked q;
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(&q);
+        gu64 *src = (gu64 *)(P.park + t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, q, tl);
+    }
+    tl.seg += cseg;
+    flush_tally(P, tl, false);
+}
+
+// Phase 2 of the tile kernel: the parked pixels, kG lanes per pixel, in park order.
 template <bool kLds, uint32_t kG>
 __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
-    const double4 *sph = sv.sph;
-    const uint32_t n = P.n_sph;
-    const float4 *filt = P.filt;
-    if (kLds) {  // pass-1 records after the shading records
-        float4 *lf = reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + n);
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lf[i] = P.filt[i];
-        __syncthreads();
-        filt = lf;
-    }
+    const float4 *filt =
+        stage_filt<kLds>(P, reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph));
     const uint32_t sub = threadIdx.x & (kG - 1u);
     Tally tl;
     uint32_t seg = 0;
@@ -978,41 +1042,7 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
         item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
         if (item >= *P.park_count) break;
         const Parked q = P.park[item];
-        const uint32_t y = P.row_begin + q.lr * P.row_step;
-        PixelState ps;
-        ps.rng = U128{q.rng_lo, q.rng_hi};
-        ps.k = q.k;
-        ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
-        const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
-        auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
-                       double &bt) -> int {
-            const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
-            int best = -1;
-            bt = 0.;
-            for (uint32_t base = 0; base < n; base += 32u * kG) {
-                uint32_t mask = 0;  // bit j: sphere base + sub + j*kG is a candidate
-#pragma unroll 8
-                for (uint32_t j = 0; j < 32u; ++j) {
-                    const uint32_t i = base + sub + j * kG;
-                    if (i < n && (!g.fast || g.pass(filt[i]))) mask |= 1u << j;
-                }
-                while (mask) {
-                    const uint32_t j = static_cast<uint32_t>(__builtin_ctz(mask));
-                    mask &= mask - 1u;
-                    ++tl.ntest;
-                    exact_test(sph, base + sub + j * kG, ox, oy, oz, dx, dy, dz, a, best, bt);
-                }
-            }
-            group_min<kG>(bt, best);
-            return best;
-        };
-        uint32_t s = 0;
-        Stamps stp;
-        trace_samples(P, sv, q.x, y, pix, ps, 0xffffffffu, s, stp, hit);
-        if (sub == 0) {
-            write_pixel(P, q.x, q.lr, ps);
-            seg += s;
-        }
+        seg += coop_pixel<kG>(P, sv, filt, q, tl);
     }
     tl.seg = seg;
     flush_tally(P, tl, false);
@@ -1056,7 +1086,7 @@ struct rtw_session {
     ShadeRec *d_shade = nullptr;
     uint4 *d_jump = nullptr;
     unsigned long long *d_counters = nullptr;
-    uint16_t *d_spill = nullptr;
+    uint32_t *d_spill = nullptr;
     size_t spill_bytes = 0;
     Parked *d_park = nullptr;  // park queue, one slot per pixel of the largest shard so far
     size_t park_cap = 0;
@@ -1254,7 +1284,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
     const size_t spill_need = cam->max_depth > kRegSlots
-                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint16_t)
+                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint32_t)
                                   : 0;
     if (spill_need > s->spill_bytes) {
         HIPCHECK(hipSetDevice(s->device));
@@ -1286,6 +1316,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.park_cursor = s->d_park_ctl + 1;
     P.pix_cursor = s->d_park_ctl + 2;
     P.park_ctl_done = s->d_park_ctl + 3;
+    P.pixels_done = s->d_park_ctl + 4;
     P.park_flag = s->d_park_flag;
     P.seeds = s->d_seeds;
     {
@@ -1339,15 +1370,16 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     if (const char *e = std::getenv("RTW_ACCEL")) mode = std::atoi(e);
     if (mode == kBvh && !s->has_bvh) mode = kScanF32;
     if (mode < kScanF64 || mode > kBvh) mode = kScanF32;
-    size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh);
-    const bool use_lds = lds <= kLdsCap;
-    if (!use_lds) lds = 0;
-    HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
-    HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 4 * sizeof(uint32_t), st));
-    HIPCHECK(hipEventRecord(s->ev0, st));
     // phase 1: persistent per-lane refill (default) or one tile per workgroup (RTW_PERSIST=0)
     bool persist = true;
     if (const char *e = std::getenv("RTW_PERSIST")) persist = std::atoi(e) != 0;
+    size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh);
+    if (persist) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);  // pass-1 records (coop groups)
+    const bool use_lds = lds <= kLdsCap;
+    if (!use_lds) lds = 0;
+    HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
+    HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 8 * sizeof(uint32_t), st));
+    HIPCHECK(hipEventRecord(s->ev0, st));
     P.order = 1;
     if (const char *e = std::getenv("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
     uint32_t grid_p = 0;
@@ -1448,6 +1480,12 @@ void collect(rtw_session *s) {
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->pending = false;
+    uint32_t ctl[8] = {};
+    HIPCHECK(hipMemcpy(ctl, s->d_park_ctl, sizeof ctl, hipMemcpyDeviceToHost));
+    if (c[7] != 0 || ctl[4] != s->last.pixels)  // never a silently incomplete image
+        throw rtw::Error(RTW_E_HIP, "render incomplete: " + std::to_string(ctl[4]) + " of " +
+                                        std::to_string(s->last.pixels) + " pixels written, " +
+                                        std::to_string(c[7]) + " queue timeouts");
 }
 
 int default_device() {
@@ -1467,7 +1505,7 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev0));
         HIPCHECK(hipEventCreate(&s->ev1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
-        HIPCHECK(hipMalloc(&s->d_park_ctl, 4 * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         upload_jump(s);
     } catch (...) {
