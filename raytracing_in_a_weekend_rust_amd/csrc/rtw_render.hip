@@ -1413,7 +1413,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
         P.n_cursor_waves = grid_p * (wpb - heavy);
-        P.rate_k = 16, P.rate_x = 8;
+        P.rate_k = 16, P.rate_x = 16;
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
