@@ -117,7 +117,8 @@ struct KParams {
     const ShadeRec *shade;      // per-sphere radius + material
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
-    uint32_t *spill;            // path-stack levels >= kRegSlots: [level - kRegSlots][pixel]
+    uint16_t *spill;            // path-stack levels >= kRegSlots, region A: [level][pixel]
+    uint16_t *spill_b;          // region B (cooperative groups): [level][park slot]
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
     struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
     uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
@@ -218,27 +219,26 @@ __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &u
 // (one u16 per pixel per level). No private/scratch memory is used: a scratch
 // array caps the waves a CU may hold.
 constexpr uint32_t kRegSlots = 8;
-// A pixel can move between workgroups (parking), so its spill entries can be
-// written on one XCD and later on another: they are write-through stores and
-// sc1 loads, never dirty L2 lines that a late write-back could replay over the
-// newer owner's entries.
+// Spill columns are owned by one lane (or one cooperative group) for a whole
+// launch: cursor lanes use column = pixel in spill region A, cooperative groups
+// column = park slot in region B. A pixel that parks on one XCD and resumes on
+// another therefore never writes bytes that the first XCD's L2 may still hold
+// dirty (the L2s are not coherent with each other), and plain cached accesses
+// stay correct.
 struct PathStack {
     uint64_t r0 = 0, r1 = 0;
     uint32_t n = 0;
-    __device__ __forceinline__ void push(uint32_t v, uint32_t *spill, uint64_t stride, uint64_t pix) {
+    __device__ __forceinline__ void push(uint32_t v, uint16_t *spill, uint64_t stride, uint64_t col) {
         if (n < 4) r0 |= static_cast<uint64_t>(v) << (16u * n);
         else if (n < kRegSlots) r1 |= static_cast<uint64_t>(v) << (16u * (n - 4u));
-        else
-            __hip_atomic_store((gu32 *)(spill + static_cast<uint64_t>(n - kRegSlots) * stride + pix), v,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else spill[static_cast<uint64_t>(n - kRegSlots) * stride + col] = static_cast<uint16_t>(v);
         ++n;
     }
-    __device__ __forceinline__ uint32_t at(uint32_t j, uint32_t *spill, uint64_t stride,
-                                           uint64_t pix) const {
+    __device__ __forceinline__ uint32_t at(uint32_t j, const uint16_t *spill, uint64_t stride,
+                                           uint64_t col) const {
         if (j < 4) return static_cast<uint32_t>(r0 >> (16u * j)) & 0xffffu;
         if (j < kRegSlots) return static_cast<uint32_t>(r1 >> (16u * (j - 4u))) & 0xffffu;
-        return __hip_atomic_load((gu32 *)(spill + static_cast<uint64_t>(j - kRegSlots) * stride + pix),
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return spill[static_cast<uint64_t>(j - kRegSlots) * stride + col];
     }
     __device__ __forceinline__ void clear() { r0 = r1 = 0, n = 0; }
 };
@@ -354,8 +354,8 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
 // path ended (sky, or depth cap -> black); then (lr, lg, lb) is the leaf colour.
 __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restrict__ sph,
                                       const ShadeRec *__restrict__ shd, int best, double bt, double a,
-                                      Path &p, U128 &rng, uint64_t pix, uint64_t stride, double &lr,
-                                      double &lg, double &lb) {
+                                      Path &p, U128 &rng, uint16_t *spill, uint64_t col, uint64_t stride,
+                                      double &lr, double &lg, double &lb) {
     lr = lg = lb = 0.;
     if (best < 0) {
         const double uy = p.dy / __builtin_sqrt(a);
@@ -390,7 +390,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
             const double rx = vx - (nx * dt) * 2., ry = vy - (ny * dt) * 2., rz = vz - (nz * dt) * 2.;
             ndx = rx + ux * M.p, ndy = ry + uy * M.p, ndz = rz + uz * M.p;
         }
-        p.stk.push(static_cast<uint32_t>(best), P.spill, stride, pix);  // attenuation row
+        p.stk.push(static_cast<uint32_t>(best), spill, stride, col);  // attenuation row
     } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
         const double ir = M.p;
         const double ratio = front ? 1. / ir : ir;
@@ -425,11 +425,11 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
 
 // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion associates
 // (camera.rs:389); then the sample's colour is added to the pixel sum.
-__device__ __forceinline__ void fold(const KParams &P, const ShadeRec *__restrict__ shd, Path &p,
-                                     uint64_t pix, uint64_t stride, double lr, double lg, double lb,
+__device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, const uint16_t *spill,
+                                     uint64_t col, uint64_t stride, double lr, double lg, double lb,
                                      PixelState &ps) {
     for (uint32_t j = p.stk.n; j-- > 0;) {
-        const ShadeRec &A = shd[p.stk.at(j, P.spill, stride, pix)];
+        const ShadeRec &A = shd[p.stk.at(j, spill, stride, col)];
         lr = A.a0 * lr;
         lg = A.a1 * lg;
         lb = A.a2 * lb;
@@ -445,8 +445,9 @@ __device__ __forceinline__ void fold(const KParams &P, const ShadeRec *__restric
 // a sample boundary (ps then holds the state to resume from).
 template <class HitFn>
 __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView &sv,
-                                              uint32_t x, uint32_t y, uint64_t pix, PixelState &ps,
-                                              uint32_t budget, uint32_t &seg, Stamps &stp, HitFn &&hit) {
+                                              uint32_t x, uint32_t y, uint16_t *spill, uint64_t col,
+                                              PixelState &ps, uint32_t budget, uint32_t &seg, Stamps &stp,
+                                              HitFn &&hit) {
     const uint32_t n_off = P.n_off;
     if (P.max_depth == 0) {  // every sample is black (no Scene::hit call)
         ps.k = n_off;
@@ -466,10 +467,10 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
         STAMP(1);
         double lr, lg, lb;
-        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, lr, lg, lb);
+        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb);
         STAMP(3);  // 3: hit record + scatter / sky
         if (done) {
-            fold(P, sv.shd, p, pix, stride, lr, lg, lb, ps);
+            fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
             if (++ps.k >= n_off) break;
             if (seg >= budget) return true;  // sample boundary: hand the rest to the coop kernel
             gen_ray(P, pl, ps.k, ps.rng, p);
@@ -695,7 +696,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
                 return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
             }
         };
-        if (trace_samples(P, sv, x, y, pix, ps, P.seg_budget, tl.seg, stp, hit)) {
+        if (trace_samples(P, sv, x, y, P.spill, pix, ps, P.seg_budget, tl.seg, stp, hit)) {
             const uint32_t slot = atomicAdd(P.park_count, 1u);
             Parked q;
             q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
@@ -799,7 +800,7 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
 template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, const Parked &q,
-                                               Tally &tl) {
+                                               uint32_t slot, Tally &tl) {
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
@@ -833,7 +834,7 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     };
     uint32_t s = 0;
     Stamps stp;
-    trace_samples(P, sv, q.x, y, pix, ps, 0xffffffffu, s, stp, hit);
+    trace_samples(P, sv, q.x, y, P.spill_b, slot, ps, 0xffffffffu, s, stp, hit);
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
         if (P.diag) {
@@ -951,8 +952,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             double bt = 0.;
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
             double cr, cg, cb;
-            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, pix, stride, cr, cg, cb)) {
-                fold(P, sv.shd, p, pix, stride, cr, cg, cb, ps);
+            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, pix, stride, cr, cg, cb)) {
+                fold(sv.shd, p, P.spill, pix, stride, cr, cg, cb, ps);
                 const bool done = ++ps.k >= P.n_off;
                 const bool park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
                 if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
@@ -1020,7 +1021,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cseg += coop_pixel<kCoopG>(P, sv, filt, q, tl);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, q, t, tl);
     }
     tl.seg += cseg;
     flush_tally(P, tl, false);
@@ -1042,7 +1043,7 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
         item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
         if (item >= *P.park_count) break;
         const Parked q = P.park[item];
-        seg += coop_pixel<kG>(P, sv, filt, q, tl);
+        seg += coop_pixel<kG>(P, sv, filt, q, item, tl);
     }
     tl.seg = seg;
     flush_tally(P, tl, false);
@@ -1086,7 +1087,7 @@ struct rtw_session {
     ShadeRec *d_shade = nullptr;
     uint4 *d_jump = nullptr;
     unsigned long long *d_counters = nullptr;
-    uint32_t *d_spill = nullptr;
+    uint16_t *d_spill = nullptr;
     size_t spill_bytes = 0;
     Parked *d_park = nullptr;  // park queue, one slot per pixel of the largest shard so far
     size_t park_cap = 0;
@@ -1284,7 +1285,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
     const size_t spill_need = cam->max_depth > kRegSlots
-                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint32_t)
+                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint16_t) * 2
                                   : 0;
     if (spill_need > s->spill_bytes) {
         HIPCHECK(hipSetDevice(s->device));
@@ -1296,6 +1297,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         s->spill_bytes = spill_need;
     }
     P.spill = s->d_spill;
+    P.spill_b = s->d_spill ? s->d_spill + spill_need / (2 * sizeof(uint16_t)) : nullptr;
     // park queue (one slot per pixel) and the per-pixel segment budget of phase 1
     const size_t npix_sh = static_cast<size_t>(sh.n_rows) * cam->img_width;
     if (npix_sh > s->park_cap) {
