@@ -13,15 +13,20 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
             -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
 
-all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check
 
-$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_accel.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OUT)/rtw_accel_build.o: $(SRC)/host/rtw_accel_build.cpp $(SRC)/rtw_accel.h
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -I$(SRC) -c $< -o $@
+
+# test infrastructure: exhaustive check of the division-free next_01 (tests/test_accel.py)
+$(OUT)/next01_check: tools/next01_check.cpp $(SRC)/rtw_numeric.h
+	@mkdir -p $(OUT)
+	$(CXX) -O2 -std=c++17 -ffp-contract=off -fno-fast-math -I$(SRC) -o $@ $< -lpthread
 
 # test infrastructure: host self-check of the BVH walk (tests/test_accel.py)
 $(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so

@@ -92,8 +92,8 @@ struct Builder {
             const uint32_t m0 = split(b, m), m1 = split(m, e);
             part = {{b, m0}, {m0, m}, {m, m1}, {m1, e}};
         }
-        const uint32_t id = static_cast<uint32_t>(out->nodes.size() / 32);
-        out->nodes.resize(out->nodes.size() + 32, 0.f);
+        const uint32_t id = static_cast<uint32_t>(out->nodes.size() / kNodeFloats);
+        out->nodes.resize(out->nodes.size() + kNodeFloats, 0.f);
         uint32_t ref[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
         double cen[4][3] = {};
         float box[6][4];
@@ -132,7 +132,7 @@ struct Builder {
             for (int t = 0; t < 4; ++t) byte |= static_cast<uint32_t>(perm[t]) << (2 * t);
             ord[o >> 2] |= byte << (8 * (o & 3));
         }
-        float *N = &out->nodes[32 * static_cast<size_t>(id)];
+        float *N = &out->nodes[kNodeFloats * static_cast<size_t>(id)];
         for (int q = 0; q < 6; ++q)
             for (int j = 0; j < 4; ++j) N[4 * q + j] = box[q][j];
         for (int j = 0; j < 4; ++j) N[24 + j] = as_f32(ref[j]);
@@ -173,7 +173,7 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     if (m == 0) return true;
     Builder b{centers, radii, r2p, rest, &out};
     b.wide(0, m, 1);
-    out.n_node = static_cast<uint32_t>(out.nodes.size() / 32);
+    out.n_node = static_cast<uint32_t>(out.nodes.size() / kNodeFloats);
     return true;
 }
 

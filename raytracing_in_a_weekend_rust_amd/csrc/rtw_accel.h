@@ -52,6 +52,11 @@ constexpr uint32_t kMaxSpheres = 32768;  // 16-bit leaf / node ids
 constexpr uint32_t kStack = 16;          // register stack: 4 x u64 of 16-bit entries
 constexpr uint32_t kEmpty = 0xffffffffu;  // empty child slot
 constexpr uint32_t kSphereBit = 0x80000000u;  // child slot holds leaf (sphere) k
+// Node stride 9 float4 (144 B): with 8 (128 B) every node starts on one of 2 of
+// the 16 four-bank slots and ds_read_b128 gathers of different nodes conflict
+// 8-way; an odd stride spreads them over all 16.
+constexpr uint32_t kNodeF4 = 9;
+constexpr uint32_t kNodeFloats = 4 * kNodeF4;
 constexpr uint32_t kMaxAlways = 16;
 constexpr uint32_t kMaxCand = 8;        // candidate list: 2 x u64 of 16-bit entries
 constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -> "always"
@@ -221,7 +226,11 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
     const bool oct_hi = r.neg >= 4u;
     for (;;) {
         ++visits;
-        const F4 *N = nodes + 8u * cur;
+#if defined(RTW_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+        // diagnostic: wave-level iterations, counted by the first active lane in bit 16+
+        if (__builtin_ctzll(__builtin_amdgcn_read_exec()) == static_cast<int>(__lane_id())) visits += 1u << 16;
+#endif
+        const F4 *N = nodes + kNodeF4 * cur;
         const F4 qlx = N[0], qhx = N[1], qly = N[2], qhy = N[3], qlz = N[4], qhz = N[5], qc = N[6], qo = N[7];
         uint32_t hit = 0;
         hit |= slab_hit<F4>(qlx.x, qhx.x, qly.x, qhy.x, qlz.x, qhz.x, r, U) ? 1u : 0u;
@@ -298,7 +307,7 @@ inline float filter_r2p(const double *c, double rr) {
 // too many "always" spheres): the kernel then scans by brute force.
 struct Bvh {
     uint32_t n_node = 0, n_leaf = 0, depth = 0;
-    std::vector<float> nodes;      // 32 floats per 4-wide node (eight float4)
+    std::vector<float> nodes;      // kNodeFloats per 4-wide node (eight float4 + pad)
     std::vector<float> leaves;     // 8 floats per leaf (two float4)
     std::vector<uint32_t> always;  // sphere indices tested exactly first, ascending
 };

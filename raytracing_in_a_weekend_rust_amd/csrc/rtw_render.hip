@@ -33,6 +33,7 @@
 
 #include "rtw_accel.h"
 #include "rtw_capi.h"
+#include "rtw_numeric.h"
 #include "host/rtw_host.h"
 #include "host/rtw_internal.h"
 
@@ -147,14 +148,15 @@ __device__ __forceinline__ void xs_step(U128 &s) {
     s.hi = hi;
 }
 // random.rs:40-52: u128 % (2^32-1) by limb folding (2^32 == 1 mod 2^32-1),
-// then an IEEE f64 divide (not a reciprocal multiply).
+// then m / 4294967295.0 correctly rounded, computed division-free
+// (rtw_numeric.h; exhaustively equal to the IEEE divide for every m).
 __device__ __forceinline__ double xs_next_01(U128 &s) {
     xs_step(s);
     uint64_t t = (s.lo & 0xffffffffull) + (s.lo >> 32) + (s.hi & 0xffffffffull) + (s.hi >> 32);
     t = (t & 0xffffffffull) + (t >> 32);
     t = (t & 0xffffffffull) + (t >> 32);
     const uint32_t m = t == 0xffffffffull ? 0u : static_cast<uint32_t>(t);
-    return static_cast<double>(m) / 4294967295.0;
+    return rtw_num::next01_of(m);
 }
 // random.rs:61-69: the child handed out by copy_reset at parent state p
 __device__ __forceinline__ U128 child_of(U128 p) {
@@ -295,7 +297,7 @@ struct SceneView {
 // LDS layout: [n] double4 sph | [n] ShadeRec | (BVH) [8 n_node] + [2 n_leaf] float4
 __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh) {
     return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
-           (bvh ? (8 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
+           (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -585,7 +587,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
                                        const float4 *__restrict__ nodes,
                                        const float4 *__restrict__ leaves, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a,
-                                       double &bt, Tally &tl) {
+                                       double &bt, Tally &tl, Stamps &stp) {
     const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
     int best = -1;
     bool brute = !g.fast;
@@ -597,6 +599,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
                 exact_test(sph, i, ox, oy, oz, dx, dy, dz, a, best, bt);
             }
         }
+        STAMP(5);  // 5: segment setup + always-spheres
         rtw_accel::WalkRay wr;
         if (P.n_leaf == 0) {
         } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
@@ -605,7 +608,9 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
             uint64_t c0 = 0, c1 = 0;
             uint32_t nc = 0;
-            if (!rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits)) {
+            const bool walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits);
+            STAMP(2);  // 2: BVH walk
+            if (!walked) {
                 brute = true;
             } else {
                 for (uint32_t j = 0; j < nc; ++j) {
@@ -637,7 +642,12 @@ __device__ __forceinline__ void flush_tally(const KParams &P, const Tally &tl, b
     if (tl.ntest) atomicAdd(&P.counters[2], static_cast<unsigned long long>(tl.ntest));
     if (tl.nwave2) atomicAdd(&P.counters[3], static_cast<unsigned long long>(tl.nwave2));
     if (tl.witer) atomicAdd(&P.counters[1], static_cast<unsigned long long>(tl.witer));
+#ifdef RTW_STAMPS  // visits carries wave-level walk iterations in bits 16+ (diagnostic build)
+    if (tl.visits & 0xffffu) atomicAdd(&P.counters[4], static_cast<unsigned long long>(tl.visits & 0xffffu));
+    if (tl.visits >> 16) atomicAdd(&P.counters[5], static_cast<unsigned long long>(tl.visits >> 16));
+#else
     if (tl.visits) atomicAdd(&P.counters[4], static_cast<unsigned long long>(tl.visits));
+#endif
     if (tl.nbrute) atomicAdd(&P.counters[5], static_cast<unsigned long long>(tl.nbrute));
     if (tl.parked) atomicAdd(&P.counters[6], static_cast<unsigned long long>(tl.parked));
 }
@@ -652,7 +662,7 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
         float4 *lf = reinterpret_cast<float4 *>(ls + n);
         if (kMode == kBvh) {
-            const uint32_t nn = 8u * P.n_node, nl = 2u * P.n_leaf;
+            const uint32_t nn = rtw_accel::kNodeF4 * P.n_node, nl = 2u * P.n_leaf;
             for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lf[i] = P.nodes[i];
             for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) lf[nn + i] = P.leaves[i];
         }
@@ -660,7 +670,7 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
         v.sph = lds;
         v.shd = ls;
         v.nodes = lf;
-        v.leaves = lf + 8u * P.n_node;
+        v.leaves = lf + rtw_accel::kNodeF4 * P.n_node;
     }
     return v;
 }
@@ -690,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                        double &bt) -> int {
             if constexpr (kMode == kBvh) {
-                return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
+                return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp);
             } else {
                 const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
                 return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -876,7 +886,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
     // pass-1 records after the scene view: after the leaves (BVH) or the shading records
     float4 *filt_lds = reinterpret_cast<float4 *>(reinterpret_cast<ShadeRec *>(lds_sph + P.n_sph) + P.n_sph);
-    if (kMode == kBvh) filt_lds += 8u * P.n_node + 2u * P.n_leaf;
+    if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf;
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
     const double4 *sph = sv.sph;
     const float4 *nodes = sv.nodes, *leaves = sv.leaves;
@@ -885,10 +895,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
     const uint64_t stride = npix;
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
+    Stamps stp_unused;
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl);
+            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp_unused);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);

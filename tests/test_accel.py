@@ -54,3 +54,14 @@ def test_ineligible_scene_reports_no_bvh(exe):
     p = subprocess.run([exe, "random:1500", "5", "10"], capture_output=True, text=True, timeout=60)
     assert p.returncode == 0
     assert json.loads(p.stdout.strip())["bvh"] is False
+
+
+def test_division_free_next01_exhaustive():
+    """rtw_numeric.h's next01_of (the device's XorShift::next_01 tail, random.rs:40-52)
+    equals the IEEE division m / 4294967295.0 for every m in [0, 2^32-2]."""
+    exe = os.path.join(ROOT, "raytracing_in_a_weekend_rust_amd", "_lib", "next01_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "-j8", "all"], check=True, capture_output=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert json.loads(p.stdout)["mismatches"] == 0

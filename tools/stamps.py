@@ -20,9 +20,11 @@ f(None, 0, C.byref(nr))
 buf = np.zeros((nr.value, 8), dtype=np.uint64)
 rc = f(buf.ctypes.data_as(C.POINTER(C.c_uint64)), nr.value, C.byref(nr))
 assert rc == 0, rc
-names = ["setup", "pass1", "pass2", "hit+scatter", "fold+next", "seg-setup"]
+names = ["setup", "hit-tail", "walk", "hit+scatter", "fold+next", "seg+always"]
 tot = buf[:, :6].sum(axis=0).astype(np.float64)
 print(f"s={s} kernel_ms={st.kernel_ms:.1f} waves={nr.value} segments={st.segments} wave_iters={st.wave_iterations}")
+print(f"walk: lane visits/segment {st.node_visits / max(1, st.segments):.2f} (wrapped 16-bit per lane: lower bound); "
+      f"wave-level walk iterations/wave-iter {st.brute_segments / max(1, st.wave_iterations):.2f}")
 for k, nme in enumerate(names):
     print(f"  {nme:12s} {tot[k]/tot.sum()*100:6.2f}%  {tot[k]/max(1,st.wave_iterations):10.0f} cyc/wave-iter")
 print(f"  total per wave-iter {tot.sum()/st.wave_iterations:.0f} cycles; waves resident-equivalent "
@@ -33,7 +35,7 @@ segmax = buf[:, 6].astype(np.float64)
 order = np.argsort(-life)
 print("per-wave lifetime (Mcycles): mean %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f; kernel %.1f Mcycles@2.4GHz"
       % (life.mean() / 1e6, np.percentile(life, 50) / 1e6, np.percentile(life, 90) / 1e6,
-         np.percentile(life, 99) / 1e6, life.max() / 1e6, st.kernel_ms * 2.4e3))
+         np.percentile(life, 99) / 1e6, life.max() / 1e6, st.kernel_ms * 2.4e6 / 1e6))
 print("per-wave max-lane segments: mean %.0f p99 %.0f max %.0f" % (segmax.mean(), np.percentile(segmax, 99), segmax.max()))
 gx = (1200 + 15) // 16
 for w in order[:8]:
