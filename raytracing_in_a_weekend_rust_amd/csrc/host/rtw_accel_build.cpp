@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <cstdlib>
 #include <vector>
 
 #include "rtw_accel.h"
@@ -37,6 +38,7 @@ struct Builder {
     std::vector<uint32_t> idx;
     Bvh *out;
     uint32_t n_leaf = 0;
+    bool median = false;
 
     void bounds(uint32_t b, uint32_t e, double lo[3], double hi[3]) const {
         for (int k = 0; k < 3; ++k) lo[k] = INFINITY, hi[k] = -INFINITY;
@@ -50,22 +52,64 @@ struct Builder {
         }
     }
 
-    // object-median split of idx[b, e) on the longest centroid axis; returns mid
-    uint32_t split(uint32_t b, uint32_t e) {
-        double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-        for (uint32_t j = b; j < e; ++j)
-            for (int k = 0; k < 3; ++k) {
-                clo[k] = std::min(clo[k], c[3 * idx[j] + k]);
-                chi[k] = std::max(chi[k], c[3 * idx[j] + k]);
-            }
-        uint32_t axis = 0;
-        for (uint32_t k = 1; k < 3; ++k)
-            if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+    // Surface-area-heuristic split of idx[b, e): for each axis, sort by centroid
+    // and sweep every cut, cost = area(left) |left| + area(right) |right|; the
+    // range is left sorted on the best axis. Returns the cut. (Object median on
+    // the longest axis when RTW_BVH_MEDIAN is set: A/B only.)
+    static double box_area(const double lo[3], const double hi[3]) {
+        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        return dx * dy + dy * dz + dz * dx;
+    }
+    void sort_axis(uint32_t b, uint32_t e, uint32_t axis) {
         std::sort(idx.begin() + b, idx.begin() + e, [&](uint32_t x, uint32_t y) {
             const double cx = c[3 * x + axis], cy = c[3 * y + axis];
             return cx < cy || (cx == cy && x < y);
         });
-        return b + (e - b) / 2;
+    }
+    uint32_t split(uint32_t b, uint32_t e) {
+        const uint32_t n = e - b;
+        if (median) {
+            double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t j = b; j < e; ++j)
+                for (int k = 0; k < 3; ++k) {
+                    clo[k] = std::min(clo[k], c[3 * idx[j] + k]);
+                    chi[k] = std::max(chi[k], c[3 * idx[j] + k]);
+                }
+            uint32_t axis = 0;
+            for (uint32_t k = 1; k < 3; ++k)
+                if (chi[k] - clo[k] > chi[axis] - clo[axis]) axis = k;
+            sort_axis(b, e, axis);
+            return b + n / 2;
+        }
+        double best = INFINITY;
+        uint32_t best_axis = 0, best_cut = b + n / 2;
+        std::vector<double> right(n + 1);
+        for (uint32_t axis = 0; axis < 3; ++axis) {
+            sort_axis(b, e, axis);
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t j = n; j-- > 0;) {  // right[j] = area of idx[b + j, e)
+                const uint32_t i = idx[b + j];
+                const double rad = std::fabs(r[i]);
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], c[3 * i + k] - rad);
+                    hi[k] = std::max(hi[k], c[3 * i + k] + rad);
+                }
+                right[j] = box_area(lo, hi);
+            }
+            for (int k = 0; k < 3; ++k) lo[k] = INFINITY, hi[k] = -INFINITY;
+            for (uint32_t j = 0; j + 1 < n; ++j) {  // cut after j: left = [b, b+j]
+                const uint32_t i = idx[b + j];
+                const double rad = std::fabs(r[i]);
+                for (int k = 0; k < 3; ++k) {
+                    lo[k] = std::min(lo[k], c[3 * i + k] - rad);
+                    hi[k] = std::max(hi[k], c[3 * i + k] + rad);
+                }
+                const double cost = box_area(lo, hi) * (j + 1) + right[j + 1] * (n - j - 1);
+                if (cost < best) best = cost, best_axis = axis, best_cut = b + j + 1;
+            }
+        }
+        sort_axis(b, e, best_axis);
+        return best_cut;
     }
 
     uint32_t leaf_record(uint32_t i) {
@@ -172,6 +216,7 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     out.n_leaf = m;
     if (m == 0) return true;
     Builder b{centers, radii, r2p, rest, &out};
+    b.median = std::getenv("RTW_BVH_MEDIAN") != nullptr;
     b.wide(0, m, 1);
     out.n_node = static_cast<uint32_t>(out.nodes.size() / kNodeFloats);
     return true;
