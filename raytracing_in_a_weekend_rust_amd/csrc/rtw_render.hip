@@ -126,6 +126,9 @@ struct KParams {
     uint32_t *park_cursor;
     U128 *seeds;                // per-pixel RNG children (persistent phase 1)
     uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
+    uint32_t *order_map;        // hand-out order of the persistent kernel (pixel per ticket) or null
+    uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base
+    uint32_t *cost_hist;        // [kCostBuckets] counts, then bucket write cursors
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
     uint32_t *park_flag;        // per park slot: 1 once the entry is published
@@ -867,6 +870,96 @@ __device__ __forceinline__ const float4 *stage_filt(const KParams &P, float4 *lf
     return lf;
 }
 
+// Hand-out order by estimated cost. rtw_cost_probe traces kProbeSamples of every
+// pixel's lattice (spread over the lattice) on a COPY of the pixel's RNG -- the
+// render itself is untouched -- and adds the segment count to the cost of the
+// pixel's 8x8 tile. Tiles are then bucketed by cost per sample (descending) and
+// laid out tile by tile (row-major inside a tile) in the order the persistent
+// kernel hands pixels out: expensive tiles start first, the cheapest fill the
+// drain, and lanes refilled together get neighbouring pixels (coherent rays).
+constexpr uint32_t kProbeSamples = 2;
+constexpr uint32_t kCostBuckets = 256;
+constexpr uint32_t kOrderTile = 8;
+struct TileGrid {
+    uint32_t tx, ty;
+    __host__ __device__ TileGrid(const KParams &P)
+        : tx((P.W + kOrderTile - 1) / kOrderTile), ty((P.n_rows + kOrderTile - 1) / kOrderTile) {}
+    __device__ uint32_t of(uint32_t x, uint32_t lr) const { return (lr / kOrderTile) * tx + x / kOrderTile; }
+    __device__ uint32_t pixels(const KParams &P, uint32_t t) const {
+        const uint32_t bx = (t % tx) * kOrderTile, by = (t / tx) * kOrderTile;
+        return min(kOrderTile, P.W - bx) * min(kOrderTile, P.n_rows - by);
+    }
+};
+template <bool kLds>
+__global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kBvh>(P, lds_sph);
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+    Tally tl;
+    Stamps stp;
+    if (i < npix) {
+        const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
+        const PixelLoc pl(P, x, P.row_begin + lr * P.row_step);
+        U128 rng = P.seeds[i];
+        uint32_t segs = 0;
+        for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
+            Path p;
+            gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p);
+            for (;;) {  // one path (no spill: depth capped below the register slots)
+                ++segs;
+                const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+                double bt = 0.;
+                const int best = bvh_hit(P, sv.sph, sv.nodes, sv.leaves, p.ox, p.oy, p.oz, p.dx, p.dy,
+                                         p.dz, a, bt, tl, stp);
+                if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
+                double cr, cg, cb;
+                shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb);
+            }
+        }
+        atomicAdd(P.cost + TileGrid(P).of(x, lr), segs);
+    }
+}
+// per tile: cost bucket (descending cost per sample) and its pixel count into the histogram
+__global__ __launch_bounds__(kBlock) void rtw_cost_bucket(const KParams P) {
+    const TileGrid tg(P);
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= tg.tx * tg.ty) return;
+    const uint32_t np = tg.pixels(P, t);
+    const uint32_t per = static_cast<uint32_t>((8ull * P.cost[t]) / (np * kProbeSamples));  // 1/8 seg/sample
+    const uint32_t b = kCostBuckets - 1u - min(per, kCostBuckets - 1u);
+    P.cost[t] = b;
+    atomicAdd(P.cost_hist + b, np);
+}
+// exclusive prefix sums of pixel counts over the buckets -> bucket write cursors
+__global__ void rtw_cost_scan(const KParams P) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t b = 0; b < kCostBuckets; ++b) {
+            const uint32_t c = P.cost_hist[b];
+            P.cost_hist[b] = acc;
+            acc += c;
+        }
+    }
+}
+// per tile: its base in the order (tiles of one bucket in any order)
+__global__ __launch_bounds__(kBlock) void rtw_cost_place(const KParams P) {
+    const TileGrid tg(P);
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= tg.tx * tg.ty) return;
+    P.cost[t] = atomicAdd(P.cost_hist + P.cost[t], tg.pixels(P, t));
+}
+// per pixel: order[tile base + row-major rank inside the tile] = pixel
+__global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
+    const TileGrid tg(P);
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= static_cast<uint64_t>(P.n_rows) * P.W) return;
+    const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
+    const uint32_t bx = (x / kOrderTile) * kOrderTile, wx = min(kOrderTile, P.W - bx);
+    const uint32_t rank = (lr % kOrderTile) * wx + (x - bx);
+    P.order_map[P.cost[tg.of(x, lr)] + rank] = static_cast<uint32_t>(i);
+}
+
 // Phase 1, persistent form, with the heavy tail folded in. Every lane of a
 // cursor wave runs one pixel at a time and, when the pixel completes, takes the
 // next pixel of the shard from a global cursor (one atomic per wave per refill).
@@ -930,12 +1023,19 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
                 if (ticket < npix) {
-                    // hand-out order: rows bottom-up when P.order == 1 (sky rows, the
-                    // cheapest in the book's scenes, go last and fill the drain)
-                    const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
-                    x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
-                    lr = P.order ? P.n_rows - 1u - tr : tr;
-                    pix = static_cast<uint64_t>(lr) * P.W + x;
+                    // hand-out order: by descending estimated cost (P.order_map,
+                    // rtw_cost_probe), so the cheapest pixels fill the drain; else
+                    // rows bottom-up when P.order == 1, or row-major
+                    if (P.order_map) {
+                        pix = P.order_map[ticket];
+                        lr = static_cast<uint32_t>(pix / P.W);
+                        x = static_cast<uint32_t>(pix - static_cast<uint64_t>(lr) * P.W);
+                    } else {
+                        const uint32_t tr = static_cast<uint32_t>(ticket / P.W);
+                        x = static_cast<uint32_t>(ticket - static_cast<uint64_t>(tr) * P.W);
+                        lr = P.order ? P.n_rows - 1u - tr : tr;
+                        pix = static_cast<uint64_t>(lr) * P.W + x;
+                    }
                     ps.rng = P.seeds[pix];
                     ps.k = 0;
                     ps.ar = ps.ag = ps.ab = 0.;
@@ -1105,6 +1205,7 @@ struct rtw_session {
     uint32_t *d_park_ctl = nullptr;  // [0] parked count, [1] phase-2 cursor, [2] pixel cursor
     U128 *d_seeds = nullptr;         // per-pixel RNG children of the current shard
     uint32_t *d_park_flag = nullptr; // per park slot publish flags
+    uint32_t *d_order = nullptr, *d_cost = nullptr, *d_cost_hist = nullptr;  // cost-ordered hand-out
     uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
     size_t diag_bytes = 0, diag_n = 0;
     int n_cu = 0;
@@ -1317,11 +1418,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (s->pending) HIPCHECK(hipEventSynchronize(s->ev1));
         dev_free(s->d_park);
         s->d_park = nullptr, s->park_cap = 0;
-        dev_free(s->d_seeds), dev_free(s->d_park_flag);
-        s->d_seeds = nullptr, s->d_park_flag = nullptr;
+        dev_free(s->d_seeds), dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost);
+        s->d_seeds = nullptr, s->d_park_flag = nullptr, s->d_order = nullptr, s->d_cost = nullptr;
         HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
         HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
         HIPCHECK(hipMalloc(&s->d_park_flag, npix_sh * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_order, npix_sh * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_cost, npix_sh * sizeof(uint32_t)));
         s->park_cap = npix_sh;
     }
     P.park = s->d_park;
@@ -1393,7 +1496,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
     HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 8 * sizeof(uint32_t), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
-    P.order = 1;
+    P.order = 2;
     if (const char *e = std::getenv("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
     uint32_t grid_p = 0;
     if (P.n_rows && persist) {
@@ -1401,6 +1504,25 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((npix + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
+        // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
+        // bottom-up, 0 row-major
+        P.order_map = nullptr;
+        if (P.order == 2 && mode == kBvh && P.max_depth > 0) {
+            P.cost = s->d_cost, P.cost_hist = s->d_cost_hist, P.order_map = s->d_order;
+            const dim3 g1(static_cast<uint32_t>((npix + kBlock - 1) / kBlock));
+            const TileGrid tg(P);
+            const dim3 gt((tg.tx * tg.ty + kBlock - 1) / kBlock);
+            HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
+            HIPCHECK(hipMemsetAsync(s->d_cost, 0, static_cast<size_t>(tg.tx) * tg.ty * sizeof(uint32_t), st));
+            const size_t lds_p = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true);
+            if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, g1, dim3(kBlock), lds_p, st, P);
+            else hipLaunchKernelGGL(rtw_cost_probe<false>, g1, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_bucket, gt, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_scan, dim3(1), dim3(64), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_place, gt, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_scatter, g1, dim3(kBlock), 0, st, P);
+            HIPCHECK(hipGetLastError());
+        }
         int pblock = kPBlock;
         if (const char *e = std::getenv("RTW_PBLOCK")) pblock = std::atoi(e) == 1024 ? 1024 : kPBlock;
         const void *fn = nullptr;
@@ -1519,6 +1641,7 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_cost_hist, kCostBuckets * sizeof(uint32_t)));
         HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         upload_jump(s);
     } catch (...) {
@@ -1569,7 +1692,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
-    dev_free(s->d_park_flag);
+    dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
