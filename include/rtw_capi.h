@@ -175,7 +175,8 @@ int rtw_session_stats(rtw_session *s, rtw_stats *out);
  * render when it ran with RTW_DIAG=1 in the environment -- for pixel p of the
  * shard (row-major), out[2p] = traced segments of the pixel in the one-lane
  * kernel, out[2p+1] = low 32 bits of the 100 MHz device real-time clock when
- * the pixel completed or parked there (0 = never ran). Returns RTW_E_CAPACITY if cap < 2 x pixels. */
+ * the pixel completed (0 = never ran); out[2 x pixels] = the clock at the persistent
+ * launch's start. Returns RTW_E_CAPACITY if cap < 2 x pixels + 4. */
 int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap);
 
 /* ---- device probes (tests) ---- */

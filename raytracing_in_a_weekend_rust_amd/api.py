@@ -263,9 +263,9 @@ class Session:
     def diag(self, n_pixels: int):
         """RTW_DIAG=1 renders: per-pixel (segments, clock/1024 at completion)."""
         import numpy as np
-        out = np.zeros(2 * n_pixels, dtype=np.uint32)
+        out = np.zeros(2 * n_pixels + 4, dtype=np.uint32)
         check(lib.rtw_session_diag(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
-        return out.reshape(n_pixels, 2)
+        return out[:2 * n_pixels].reshape(n_pixels, 2), int(out[2 * n_pixels])
 
     def close(self):
         if self.h:

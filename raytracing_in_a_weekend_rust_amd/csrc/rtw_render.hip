@@ -50,7 +50,7 @@ constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
 constexpr int kCounters = 8;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
-constexpr uint32_t kHeavyPerBlock = 1;  // priority waves per persistent workgroup (parked pixels)
+constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 
 // Scene::hit strategies (one kernel instantiation each)
@@ -972,8 +972,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
 // cursor ran dry. Groups claim queue tickets in order and wait for a claimed
 // ticket to be published; they stop once every cursor wave has signalled that it
 // parks no more and their ticket lies past the final queue length.
-constexpr uint32_t kCoopG = 16;
-template <bool kLds, int kMode, int kThreads>
+template <bool kLds, int kMode, int kThreads, uint32_t kCoopG = 16>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
@@ -999,6 +998,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         }
     };
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    if (P.diag && blockIdx.x == 0 && threadIdx.x == 0)  // diagnostic: launch start after the pixels
+        P.diag[2 * npix] = static_cast<uint32_t>(t_start);
     if (heavy_wave) {
         __builtin_amdgcn_s_setprio(3);
     } else {
@@ -1462,7 +1463,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.diag = nullptr;
     if (const char *e = std::getenv("RTW_DIAG")) {
         if (std::atoi(e) != 0) {
-            const size_t need = static_cast<size_t>(sh.n_rows) * cam->img_width * 2 * sizeof(uint32_t);
+            const size_t need = (static_cast<size_t>(sh.n_rows) * cam->img_width * 2 + 4) * sizeof(uint32_t);
             if (need > s->diag_bytes) {
                 HIPCHECK(hipSetDevice(s->device));
                 HIPCHECK(hipDeviceSynchronize());
@@ -1525,11 +1526,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         }
         int pblock = kPBlock;
         if (const char *e = std::getenv("RTW_PBLOCK")) pblock = std::atoi(e) == 1024 ? 1024 : kPBlock;
+        int coop_g = 64;  // lanes per parked pixel in the persistent drain (RTW_COOPG=16: 4 per wave)
+        if (const char *e = std::getenv("RTW_COOPG")) coop_g = std::atoi(e) == 16 ? 16 : 64;
         const void *fn = nullptr;
 #define RTW_PFN(L, M, T) reinterpret_cast<const void *>(&rtw_render_persist<L, M, T>)
         if (pblock == 1024) {
             if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(true, kScanF32, 1024) : RTW_PFN(true, kScanF64, 1024);
             else fn = mode == kBvh ? RTW_PFN(false, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(false, kScanF32, 1024) : RTW_PFN(false, kScanF64, 1024);
+        } else if (coop_g == 64 && use_lds && mode == kBvh) {
+            fn = reinterpret_cast<const void *>(&rtw_render_persist<true, kBvh, kPBlock, 64>);
         } else {
             if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(true, kScanF32, kPBlock) : RTW_PFN(true, kScanF64, kPBlock);
             else fn = mode == kBvh ? RTW_PFN(false, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(false, kScanF32, kPBlock) : RTW_PFN(false, kScanF64, kPBlock);

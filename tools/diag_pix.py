@@ -17,11 +17,11 @@ sess.set_scene(sph, n, mt, nm)
 fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0")
 sess.render(cam.raw, S, seed, fb.data_ptr())
 st = sess.stats()
-d = sess.diag(W * H)
+d, t0 = sess.diag(W * H)
 seg = d[:, 0].astype(np.float64) / (S * S)
 t = d[:, 1].astype(np.float64)
 ran = d[:, 1] > 0
-t = (t - t[ran].min()) / 1e5  # ms of the 100 MHz real-time clock
+t = (t - (t0 if t0 else t[ran].min())) / 1e5  # ms since the launch (100 MHz real-time clock)
 print(f"kernel {st.kernel_ms:.1f} ms parked {st.parked_pixels} budget_x {os.environ.get('RTW_BUDGET_X')}")
 print("seg/sample percentiles 50/90/99/99.9/99.99/max:",
       [round(float(np.percentile(seg, q)), 2) for q in (50, 90, 99, 99.9, 99.99)], round(float(seg.max()), 2))
