@@ -119,7 +119,8 @@ struct KParams {
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
     uint16_t *spill;            // path-stack levels >= kRegSlots, region A: [level][pixel]
-    uint16_t *spill_b;          // region B (cooperative groups): [level][park slot]
+    uint16_t *spill_b;          // region B (cooperative groups): [level][column]
+    uint64_t spill_stride;      // columns per level: max(pixels, persistent lanes)
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
     struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
     uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
@@ -460,7 +461,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
     }
     if (ps.k >= n_off) return false;
     const PixelLoc pl(P, x, y);
-    const uint64_t stride = static_cast<uint64_t>(P.n_rows) * P.W;
+    const uint64_t stride = P.spill_stride;
     Path p;
     gen_ray(P, pl, ps.k, ps.rng, p);
     STAMP(0);  // 0: seed jump + pixel setup
@@ -813,7 +814,7 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
 template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, const Parked &q,
-                                               uint32_t slot, Tally &tl) {
+                                               uint64_t col, Tally &tl) {
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
@@ -847,7 +848,7 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     };
     uint32_t s = 0;
     Stamps stp;
-    trace_samples(P, sv, q.x, y, P.spill_b, slot, ps, 0xffffffffu, s, stp, hit);
+    trace_samples(P, sv, q.x, y, P.spill_b, col, ps, 0xffffffffu, s, stp, hit);
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
         if (P.diag) {
@@ -985,7 +986,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     Tally tl;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
-    const uint64_t stride = npix;
+    const uint64_t stride = P.spill_stride;
+    // spill column of this lane for the whole launch: consecutive lanes of a wave
+    // share L2 lines, and the live columns stay dense
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
     Stamps stp_unused;
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
@@ -1064,8 +1068,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             double bt = 0.;
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
             double cr, cg, cb;
-            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, pix, stride, cr, cg, cb)) {
-                fold(sv.shd, p, P.spill, pix, stride, cr, cg, cb, ps);
+            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb)) {
+                fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb, ps);
                 const bool done = ++ps.k >= P.n_off;
                 const bool park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
                 if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
@@ -1133,7 +1137,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cseg += coop_pixel<kCoopG>(P, sv, filt, q, t, tl);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl);
     }
     tl.seg += cseg;
     flush_tally(P, tl, false);
@@ -1397,8 +1401,12 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.jump = s->d_jump;
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
+    // path-stack spill: 2 regions x (max_depth - kRegSlots) levels x columns (u16);
+    // columns = pixels (tile kernel), persistent lanes / drain groups (persistent)
+    const uint64_t spill_cols = std::max<uint64_t>(static_cast<uint64_t>(sh.n_rows) * cam->img_width,
+                                                   static_cast<uint64_t>(s->n_cu > 0 ? s->n_cu : 256) * 4 * 1024);
     const size_t spill_need = cam->max_depth > kRegSlots
-                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * sh.n_rows * cam->img_width * sizeof(uint16_t) * 2
+                                  ? static_cast<size_t>(cam->max_depth - kRegSlots) * spill_cols * sizeof(uint16_t) * 2
                                   : 0;
     if (spill_need > s->spill_bytes) {
         HIPCHECK(hipSetDevice(s->device));
@@ -1411,6 +1419,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
     P.spill = s->d_spill;
     P.spill_b = s->d_spill ? s->d_spill + spill_need / (2 * sizeof(uint16_t)) : nullptr;
+    P.spill_stride = spill_cols;
     // park queue (one slot per pixel) and the per-pixel segment budget of phase 1
     const size_t npix_sh = static_cast<size_t>(sh.n_rows) * cam->img_width;
     if (npix_sh > s->park_cap) {
