@@ -138,7 +138,7 @@ struct Builder {
         }
         const uint32_t id = static_cast<uint32_t>(out->nodes.size() / kNodeFloats);
         out->nodes.resize(out->nodes.size() + kNodeFloats, 0.f);
-        uint32_t ref[4] = {kEmpty, kEmpty, kEmpty, kEmpty};
+        uint32_t ref[4] = {kEmpty, kEmpty, kEmpty, kEmpty}, masks = 0;
         double cen[4][3] = {};
         float box[6][4];
         for (int q = 0; q < 6; ++q)
@@ -157,7 +157,9 @@ struct Builder {
         }
         for (size_t j = 0; j < part.size(); ++j) {
             const uint32_t pb = part[j].first, pe = part[j].second;
-            ref[j] = pe - pb == 1 ? (kSphereBit | leaf_record(idx[pb])) : wide(pb, pe, depth + 1);
+            const bool leaf = pe - pb == 1;
+            ref[j] = leaf ? leaf_record(idx[pb]) : wide(pb, pe, depth + 1);
+            masks |= (1u << j) | (leaf ? 1u << (4 + j) : 0u);
         }
         // near-to-far child order per ray octant (bit k set: direction k < 0)
         uint32_t ord[2] = {0, 0};
@@ -179,7 +181,10 @@ struct Builder {
         float *N = &out->nodes[kNodeFloats * static_cast<size_t>(id)];
         for (int q = 0; q < 6; ++q)
             for (int j = 0; j < 4; ++j) N[4 * q + j] = box[q][j];
-        for (int j = 0; j < 4; ++j) N[24 + j] = as_f32(ref[j]);
+        uint32_t packed[2] = {0, 0};
+        for (int j = 0; j < 4; ++j)
+            if (ref[j] != kEmpty) packed[j >> 1] |= (ref[j] & 0xffffu) << (16 * (j & 1));
+        N[24] = as_f32(packed[0]), N[25] = as_f32(packed[1]), N[26] = as_f32(masks), N[27] = 0.f;
         N[28] = as_f32(ord[0]), N[29] = as_f32(ord[1]), N[30] = 0.f, N[31] = 0.f;
         return id;
     }

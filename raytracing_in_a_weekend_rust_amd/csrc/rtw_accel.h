@@ -50,8 +50,7 @@ constexpr float kDirFloor = 9.094947017729282e-13f;  // 2^-40: |e_i| clamp befor
 constexpr float kGuardBvh = 1e8f;       // |origin| beyond -> brute force for the segment
 constexpr uint32_t kMaxSpheres = 32768;  // 16-bit leaf / node ids
 constexpr uint32_t kStack = 16;          // register stack: 4 x u64 of 16-bit entries
-constexpr uint32_t kEmpty = 0xffffffffu;  // empty child slot
-constexpr uint32_t kSphereBit = 0x80000000u;  // child slot holds leaf (sphere) k
+constexpr uint32_t kEmpty = 0xffffffffu;  // "no node"
 // Node stride 9 float4 (144 B): with 8 (128 B) every node starts on one of 2 of
 // the 16 four-bank slots and ds_read_b128 gathers of different nodes conflict
 // 8-way; an odd stride spreads them over all 16.
@@ -64,7 +63,8 @@ constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -
 // Node (128 B, eight float4; 4-wide, children in the parent):
 //   q0..q5 = lo.x[4], hi.x[4], lo.y[4], hi.y[4], lo.z[4], hi.z[4] (padded boxes
 //   of the 4 children; an empty slot has every plane at +inf and is never hit),
-//   q6 = child refs (inner node id, kSphereBit | leaf k, or kEmpty),
+//   q6.x/.y = child refs, 16 bits each (slot j in bits 16 (j & 1) of q6[j >> 1]):
+//   inner node id or leaf k; q6.z = slot masks: bits 0-3 occupied, bits 4-7 leaf,
 //   q7.x/.y = near-to-far child order per ray octant: byte o (octant bit k set
 //   = direction k negative) holds 4 2-bit slot indices, nearest first.
 // Leaf (32 B, two float4): {cx, cy, cz, R2'} (the pass-1 filter record) and
@@ -212,11 +212,12 @@ RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
 
 // Collects the leaves (leaf-order ids) the walk cannot rule out. Each iteration
 // takes one 4-wide node, tests its 4 child boxes, runs the leaf filter on hit
-// sphere children, continues with the nearest hit inner child and pushes the
-// other hit inner children (register stack, 16 entries). U (distance units along
-// e32) is the running cut; the caller seeds it from the "always" spheres.
-// Returns false on candidate-list or stack overflow (caller brute-forces).
-// `visits` counts loop iterations (node visits).
+// leaf children, continues with the nearest hit inner child and pushes the
+// other hit inner children (register stack of 16-bit ids, 16 entries, pushed
+// k - 1 at a time by one variable shift). U (distance units along e32) is the
+// running cut; the caller seeds it from the "always" spheres. Returns false on
+// candidate-list or stack overflow (caller brute-forces). `visits` counts loop
+// iterations (node visits).
 template <typename F4>
 RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
                  float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits) {
@@ -237,37 +238,41 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         hit |= slab_hit<F4>(qlx.y, qhx.y, qly.y, qhy.y, qlz.y, qhz.y, r, U) ? 2u : 0u;
         hit |= slab_hit<F4>(qlx.z, qhx.z, qly.z, qhy.z, qlz.z, qhz.z, r, U) ? 4u : 0u;
         hit |= slab_hit<F4>(qlx.w, qhx.w, qly.w, qhy.w, qlz.w, qhz.w, r, U) ? 8u : 0u;
-        const uint32_t ref[4] = {as_u32(qc.x), as_u32(qc.y), as_u32(qc.z), as_u32(qc.w)};
-        for (uint32_t j = 0; j < 4; ++j)
-            if (ref[j] == kEmpty) hit &= ~(1u << j);
-        // sphere children first: they may tighten U for the inner children
-        uint32_t smask = 0;
-        for (uint32_t j = 0; j < 4; ++j)
-            if ((hit >> j) & 1u && (ref[j] & kSphereBit)) smask |= 1u << j;
-        hit &= ~smask;
-        while (smask) {
-            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(smask));
-            smask &= smask - 1u;
-            if (!leaf_test(leaves, ref[j] & 0xffffu, r, U, c0, c1, nc)) return false;
+        const uint32_t r01 = as_u32(qc.x), r23 = as_u32(qc.y), masks = as_u32(qc.z);
+        hit &= masks;
+        // leaf children first: they may tighten U for the inner children
+        uint32_t lmask = hit & (masks >> 4);
+        const uint32_t inner = hit & ~lmask & 15u;
+        while (lmask) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
+            lmask &= lmask - 1u;
+            const uint32_t k = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
+            if (!leaf_test(leaves, k, r, U, c0, c1, nc)) return false;
         }
-        // inner children, far to near: push all but the nearest, continue there
+        // hit inner children packed near to far: L (16 bits each), count nk
         const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
-        uint32_t next = kEmpty;
-        for (int t = 3; t >= 0; --t) {
-            const uint32_t j = (ord >> (2 * t)) & 3u;
-            if ((hit >> j) & 1u) {
-                if (next != kEmpty) {
-                    if (sp >= kStack) return false;
-                    s3 = (s3 << 16) | (s2 >> 48);
-                    s2 = (s2 << 16) | (s1 >> 48);
-                    s1 = (s1 << 16) | (s0 >> 48);
-                    s0 = (s0 << 16) | next;
-                    ++sp;
-                }
-                next = ref[j];
-            }
+        uint64_t L = 0;
+        uint32_t nk = 0;
+        for (uint32_t t = 0; t < 4; ++t) {
+            const uint32_t j = (ord >> (2u * t)) & 3u;
+            const uint32_t id = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
+            const uint32_t h = (inner >> j) & 1u;
+            L |= static_cast<uint64_t>(h ? id : 0u) << (16u * nk);
+            nk += h;
         }
-        if (next == kEmpty) {
+        uint32_t next;
+        if (nk) {
+            // continue with the nearest, push the other nk - 1 (nearest on top)
+            const uint32_t m = nk - 1u;
+            if (sp + m > kStack) return false;
+            const uint32_t sh = 16u * m;  // 0..48
+            s3 = (s3 << sh) | ((s2 >> 1) >> (63u - sh));
+            s2 = (s2 << sh) | ((s1 >> 1) >> (63u - sh));
+            s1 = (s1 << sh) | ((s0 >> 1) >> (63u - sh));
+            s0 = (s0 << sh) | (L >> 16);
+            sp += m;
+            next = static_cast<uint32_t>(L & 0xffffu);
+        } else {
             if (sp == 0) break;
             next = static_cast<uint32_t>(s0 & 0xffffu);
             s0 = (s0 >> 16) | (s1 << 48);

@@ -2,7 +2,7 @@
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp PYTHONPATH=.
-OUT=gpurun_out/sweep
+OUT=${SWEEP_OUT:-gpurun_out/sweep}
 mkdir -p $OUT
 for cfg in ${CFGS:-"2:6:64:768" "2:10:64:768" "2:6:64:1024" "2:0:64:768"}; do
   IFS=: read a b c pb rx hv cg <<< "$cfg"
