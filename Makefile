@@ -9,7 +9,7 @@ PKG := raytracing_in_a_weekend_rust_amd
 SRC := $(PKG)/csrc
 OUT := $(PKG)/_lib
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-            -Wall -Iinclude -I$(SRC) -I$(SRC)/host
+            -Wall -Iinclude -I$(SRC) -I$(SRC)/host $(EXTRA)
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
             -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
 

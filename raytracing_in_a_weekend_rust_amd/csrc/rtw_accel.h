@@ -210,19 +210,72 @@ RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     return true;
 }
 
+// Traversal stacks of 16-bit node ids (LIFO, kStack entries). push(L, m): the
+// m entries packed in L (16 bits each, bits 0.. nearest) go on top so that the
+// nearest is popped first.
+// RegStack: 4 x u64 in registers, a push of m entries is one variable shift.
+struct RegStack {
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint32_t sp = 0;
+    RTW_HD bool push(uint64_t L, uint32_t m) {
+        if (sp + m > kStack) return false;
+        const uint32_t sh = 16u * m;  // 0..48
+        s3 = (s3 << sh) | ((s2 >> 1) >> (63u - sh));
+        s2 = (s2 << sh) | ((s1 >> 1) >> (63u - sh));
+        s1 = (s1 << sh) | ((s0 >> 1) >> (63u - sh));
+        s0 = (s0 << sh) | L;
+        sp += m;
+        return true;
+    }
+    RTW_HD bool pop(uint32_t &next) {
+        if (sp == 0) return false;
+        next = static_cast<uint32_t>(s0 & 0xffffu);
+        s0 = (s0 >> 16) | (s1 << 48);
+        s1 = (s1 >> 16) | (s2 << 48);
+        s2 = (s2 >> 16) | (s3 << 48);
+        s3 >>= 16;
+        --sp;
+        return true;
+    }
+};
+#if defined(__HIPCC__)
+// LdsStack (device): the top entry in a register, the rest in a per-lane LDS
+// column (entry k at col[k * stride], u16). A pop hands out the register and
+// reloads it from LDS -- the load completes while the next node is tested.
+struct LdsStack {
+    uint16_t *col;
+    uint32_t stride, n = 0, top = 0;  // n: entries in LDS; top valid iff sp > 0
+    uint32_t sp = 0;
+    __device__ LdsStack(uint16_t *c, uint32_t s) : col(c), stride(s) {}
+    __device__ bool push(uint64_t L, uint32_t m) {
+        if (sp + m > kStack) return false;
+        if (m == 0) return true;
+        if (sp) col[n++ * stride] = static_cast<uint16_t>(top);
+        for (uint32_t i = m - 1u; i > 0; --i) col[n++ * stride] = static_cast<uint16_t>(L >> (16u * i));
+        top = static_cast<uint32_t>(L & 0xffffu);
+        sp += m;
+        return true;
+    }
+    __device__ bool pop(uint32_t &next) {
+        if (sp == 0) return false;
+        next = top;
+        if (--sp) top = col[--n * stride];
+        return true;
+    }
+};
+#endif
+
 // Collects the leaves (leaf-order ids) the walk cannot rule out. Each iteration
 // takes one 4-wide node, tests its 4 child boxes, runs the leaf filter on hit
 // leaf children, continues with the nearest hit inner child and pushes the
-// other hit inner children (register stack of 16-bit ids, 16 entries, pushed
-// k - 1 at a time by one variable shift). U (distance units along e32) is the
-// running cut; the caller seeds it from the "always" spheres. Returns false on
-// candidate-list or stack overflow (caller brute-forces). `visits` counts loop
-// iterations (node visits).
-template <typename F4>
+// other hit inner children (k - 1 at a time). U (distance units along e32) is
+// the running cut; the caller seeds it from the "always" spheres. Returns false
+// on candidate-list or stack overflow (caller brute-forces). `visits` counts
+// loop iterations (node visits).
+template <typename F4, typename Stack>
 RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
-                 float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits) {
-    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    uint32_t sp = 0, cur = 0;
+                 float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits, Stack &stk) {
+    uint32_t cur = 0;
     const uint32_t oct_shift = 8u * (r.neg & 3u);
     const bool oct_hi = r.neg >= 4u;
     for (;;) {
@@ -260,28 +313,12 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
             L |= static_cast<uint64_t>(h ? id : 0u) << (16u * nk);
             nk += h;
         }
-        uint32_t next;
-        if (nk) {
-            // continue with the nearest, push the other nk - 1 (nearest on top)
-            const uint32_t m = nk - 1u;
-            if (sp + m > kStack) return false;
-            const uint32_t sh = 16u * m;  // 0..48
-            s3 = (s3 << sh) | ((s2 >> 1) >> (63u - sh));
-            s2 = (s2 << sh) | ((s1 >> 1) >> (63u - sh));
-            s1 = (s1 << sh) | ((s0 >> 1) >> (63u - sh));
-            s0 = (s0 << sh) | (L >> 16);
-            sp += m;
-            next = static_cast<uint32_t>(L & 0xffffu);
-        } else {
-            if (sp == 0) break;
-            next = static_cast<uint32_t>(s0 & 0xffffu);
-            s0 = (s0 >> 16) | (s1 << 48);
-            s1 = (s1 >> 16) | (s2 << 48);
-            s2 = (s2 >> 16) | (s3 << 48);
-            s3 >>= 16;
-            --sp;
+        if (nk) {  // continue with the nearest, push the other nk - 1
+            if (!stk.push(L >> 16, nk - 1u)) return false;
+            cur = static_cast<uint32_t>(L & 0xffffu);
+        } else if (!stk.pop(cur)) {
+            break;
         }
-        cur = next;
     }
     return true;
 }

@@ -41,8 +41,9 @@ namespace {
 
 constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 // persistent phase 1: one workgroup per CU shares one LDS copy of the scene;
-// 768 threads = 3 waves per SIMD at the BVH kernel's ~160 VGPRs (1024 forces
-// 128 VGPRs and spills); RTW_PBLOCK=1024 selects the 4-wave build for A/B.
+// 768 threads = 3 waves per SIMD at the BVH kernel's ~150 VGPRs. (A 1024-thread
+// build fits 128 VGPRs with the per-lane LDS areas and few spills, but measured
+// slower: bulk throughput no better, drain groups slower.)
 constexpr int kPBlock = 768;
 constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
@@ -108,7 +109,7 @@ struct KParams {
     uint32_t n_node, n_leaf, n_always, seg_budget;
     uint32_t order, heavy_per_block;
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
-    uint32_t n_cursor_waves, _pad4;
+    uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -122,6 +123,7 @@ struct KParams {
     uint16_t *spill_b;          // region B (cooperative groups): [level][column]
     uint64_t spill_stride;      // columns per level: max(pixels, persistent lanes)
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
+    uint64_t *stamps_coop;      // RTW_STAMPS builds only: phase-2 waves [wave][8]
     struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
     uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
     uint32_t *park_cursor;
@@ -303,6 +305,11 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
     return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
            (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
 }
+// Persistent kernel, per-lane LDS areas after the scene view: the running pixel
+// sum (3 x f64 columns) and the BVH walk stack (kStack x u16 columns).
+__host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
+    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kStack * sizeof(uint16_t));
+}
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
 struct Path {
@@ -432,8 +439,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
 // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion associates
 // (camera.rs:389); then the sample's colour is added to the pixel sum.
 __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, const uint16_t *spill,
-                                     uint64_t col, uint64_t stride, double lr, double lg, double lb,
-                                     PixelState &ps) {
+                                     uint64_t col, uint64_t stride, double &lr, double &lg, double &lb) {
     for (uint32_t j = p.stk.n; j-- > 0;) {
         const ShadeRec &A = shd[p.stk.at(j, spill, stride, col)];
         lr = A.a0 * lr;
@@ -441,6 +447,11 @@ __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, 
         lb = A.a2 * lb;
     }
     p.stk.clear();
+}
+__device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, const uint16_t *spill,
+                                     uint64_t col, uint64_t stride, double lr, double lg, double lb,
+                                     PixelState &ps) {
+    fold(shd, p, spill, col, stride, lr, lg, lb);
     ps.ar = ps.ar + lr, ps.ag = ps.ag + lg, ps.ab = ps.ab + lb;
 }
 
@@ -587,11 +598,12 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 
 // Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
 // exact candidates, the cut check; anything unproven falls back to the scan.
+template <bool kLdsStack = false>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restrict__ sph,
                                        const float4 *__restrict__ nodes,
                                        const float4 *__restrict__ leaves, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a,
-                                       double &bt, Tally &tl, Stamps &stp) {
+                                       double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr) {
     const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
     int best = -1;
     bool brute = !g.fast;
@@ -612,7 +624,14 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
             uint64_t c0 = 0, c1 = 0;
             uint32_t nc = 0;
-            const bool walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits);
+            bool walked;
+            if constexpr (kLdsStack) {
+                rtw_accel::LdsStack stk(scol, blockDim.x);
+                walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
+            } else {
+                rtw_accel::RegStack stk;
+                walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
+            }
             STAMP(2);  // 2: BVH walk
             if (!walked) {
                 brute = true;
@@ -814,7 +833,7 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
 template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, const Parked &q,
-                                               uint64_t col, Tally &tl) {
+                                               uint64_t col, Tally &tl, Stamps &stp) {
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
@@ -831,23 +850,25 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         bt = 0.;
         for (uint32_t base = 0; base < n; base += 32u * kG) {
             uint32_t mask = 0;  // bit j: sphere base + sub + j*kG is a candidate
+            const uint32_t jn = min(32u, (n - base + kG - 1u) / kG);  // group-uniform
 #pragma unroll 8
-            for (uint32_t j = 0; j < 32u; ++j) {
+            for (uint32_t j = 0; j < jn; ++j) {
                 const uint32_t i = base + sub + j * kG;
                 if (i < n && (!g.fast || g.pass(filt[i]))) mask |= 1u << j;
             }
+            STAMP(5);  // coop: segment setup + filter
             while (mask) {
                 const uint32_t j = static_cast<uint32_t>(__builtin_ctz(mask));
                 mask &= mask - 1u;
                 ++tl.ntest;
                 exact_test(sph, base + sub + j * kG, ox, oy, oz, dx, dy, dz, a, best, bt);
             }
+            STAMP(2);  // coop: exact tests
         }
         group_min<kG>(bt, best);
         return best;
     };
     uint32_t s = 0;
-    Stamps stp;
     trace_samples(P, sv, q.x, y, P.spill_b, col, ps, 0xffffffffu, s, stp, hit);
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
@@ -973,7 +994,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
 // cursor ran dry. Groups claim queue tickets in order and wait for a claimed
 // ticket to be published; they stop once every cursor wave has signalled that it
 // parks no more and their ticket lies past the final queue length.
-template <bool kLds, int kMode, int kThreads, uint32_t kCoopG = 16>
+template <bool kLds, int kMode, uint32_t kThreads, uint32_t kCoopG = 16>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
@@ -981,6 +1002,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     float4 *filt_lds = reinterpret_cast<float4 *>(reinterpret_cast<ShadeRec *>(lds_sph + P.n_sph) + P.n_sph);
     if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf;
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
+    // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
+    // read and written once per sample) and the BVH walk stack (kStack u16
+    // columns) -- state that would otherwise hold ~12 VGPRs through the walk
+    double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
+    uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);
     const double4 *sph = sv.sph;
     const float4 *nodes = sv.nodes, *leaves = sv.leaves;
     Tally tl;
@@ -991,11 +1017,13 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     // share L2 lines, and the live columns stay dense
     const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
+
     Stamps stp_unused;
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp_unused);
+            return bvh_hit<true>(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp_unused,
+                                 lane_stk + threadIdx.x);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -1013,7 +1041,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         uint64_t pix = 0;
         PixelState ps;
         Path p;
-        PixelLoc pl;
         for (;;) {
             {  // the wave's first active lane counts the wave-level iteration
                 const uint64_t exm = __builtin_amdgcn_read_exec();
@@ -1043,14 +1070,13 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     }
                     ps.rng = P.seeds[pix];
                     ps.k = 0;
-                    ps.ar = ps.ag = ps.ab = 0.;
+                    acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
                     if (P.max_depth == 0) {  // every sample black, no Scene::hit call
                         ps.k = P.n_off;
                         write_pixel(P, x, lr, ps);
                     } else {
-                        pl = PixelLoc(P, x, P.row_begin + lr * P.row_step);
-                        gen_ray(P, pl, 0, ps.rng, p);
+                        gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), 0, ps.rng, p);
                         need = false;
                     }
                 } else {
@@ -1069,7 +1095,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
             double cr, cg, cb;
             if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb)) {
-                fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb, ps);
+                fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
+                acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 const bool done = ++ps.k >= P.n_off;
                 const bool park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
                 if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
@@ -1078,6 +1105,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                                        static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
+                ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
                 if (done) {
                     write_pixel(P, x, lr, ps);
                     need = true;
@@ -1090,7 +1118,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     ++tl.parked;
                     need = true;
                 } else {
-                    gen_ray(P, pl, ps.k, ps.rng, p);
+                    gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, ps.rng, p);
                 }
             }
         }
@@ -1137,7 +1165,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
     }
     tl.seg += cseg;
     flush_tally(P, tl, false);
@@ -1152,6 +1180,7 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
         stage_filt<kLds>(P, reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph));
     const uint32_t sub = threadIdx.x & (kG - 1u);
     Tally tl;
+    Stamps stp;
     uint32_t seg = 0;
     for (;;) {
         uint32_t item = 0;
@@ -1159,8 +1188,15 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
         item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
         if (item >= *P.park_count) break;
         const Parked q = P.park[item];
-        seg += coop_pixel<kG>(P, sv, filt, q, item, tl);
+        seg += coop_pixel<kG>(P, sv, filt, q, item, tl, stp);
     }
+#ifdef RTW_STAMPS
+    if ((threadIdx.x & 63u) == 0) {  // diagnostic: per-wave rows after the tile kernel's
+        uint64_t *row = P.stamps_coop + (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64u) + threadIdx.x / 64u) * 8;
+        for (int k = 0; k < 6; ++k) row[k] = stp.acc[k];
+        row[6] = seg, row[7] = stamp_now();
+    }
+#endif
     tl.seg = seg;
     flush_tally(P, tl, false);
 }
@@ -1454,7 +1490,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
 #ifdef RTW_STAMPS
     {
-        const size_t nw = static_cast<size_t>((P.W + kTile - 1) / kTile) * ((sh.n_rows + kTile - 1) / kTile) * 4;
+        const size_t nt = static_cast<size_t>((P.W + kTile - 1) / kTile) * ((sh.n_rows + kTile - 1) / kTile) * 4;
+        const size_t nw = nt + static_cast<size_t>(kCoopBlocks) * (kBlock / 64);  // + phase-2 waves
         static uint64_t *d_st = nullptr;
         static size_t cap = 0;
         if (nw * 64 > cap) {
@@ -1464,6 +1501,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         }
         HIPCHECK(hipMemset(d_st, 0, nw * 64));
         P.stamps = d_st;
+        P.stamps_coop = d_st + nt * 8;
         stamp_buf() = d_st;
         stamp_n() = nw;
     }
@@ -1533,20 +1571,22 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             hipLaunchKernelGGL(rtw_cost_scatter, g1, dim3(kBlock), 0, st, P);
             HIPCHECK(hipGetLastError());
         }
-        int pblock = kPBlock;
-        if (const char *e = std::getenv("RTW_PBLOCK")) pblock = std::atoi(e) == 1024 ? 1024 : kPBlock;
+        const int pblock = kPBlock;
         int coop_g = 64;  // lanes per parked pixel in the persistent drain (RTW_COOPG=16: 4 per wave)
         if (const char *e = std::getenv("RTW_COOPG")) coop_g = std::atoi(e) == 16 ? 16 : 64;
+        // LDS: the scene view + pass-1 records when they fit beside the per-lane areas
+        const size_t lane_b = lane_lds_bytes(kPBlock);
+        bool lds_scene = use_lds && lds + lane_b <= kLdsCap;
+        P.lane_lds_off = lds_scene ? static_cast<uint32_t>((lds + 15) & ~size_t(15)) : 0u;
+        lds = P.lane_lds_off + lane_b;
         const void *fn = nullptr;
-#define RTW_PFN(L, M, T) reinterpret_cast<const void *>(&rtw_render_persist<L, M, T>)
-        if (pblock == 1024) {
-            if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(true, kScanF32, 1024) : RTW_PFN(true, kScanF64, 1024);
-            else fn = mode == kBvh ? RTW_PFN(false, kBvh, 1024) : mode == kScanF32 ? RTW_PFN(false, kScanF32, 1024) : RTW_PFN(false, kScanF64, 1024);
-        } else if (coop_g == 64 && use_lds && mode == kBvh) {
+#define RTW_PFN(L, M) reinterpret_cast<const void *>(&rtw_render_persist<L, M, kPBlock>)
+        if (coop_g == 64 && lds_scene && mode == kBvh) {
             fn = reinterpret_cast<const void *>(&rtw_render_persist<true, kBvh, kPBlock, 64>);
+        } else if (lds_scene) {
+            fn = mode == kBvh ? RTW_PFN(true, kBvh) : mode == kScanF32 ? RTW_PFN(true, kScanF32) : RTW_PFN(true, kScanF64);
         } else {
-            if (use_lds) fn = mode == kBvh ? RTW_PFN(true, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(true, kScanF32, kPBlock) : RTW_PFN(true, kScanF64, kPBlock);
-            else fn = mode == kBvh ? RTW_PFN(false, kBvh, kPBlock) : mode == kScanF32 ? RTW_PFN(false, kScanF32, kPBlock) : RTW_PFN(false, kScanF64, kPBlock);
+            fn = mode == kBvh ? RTW_PFN(false, kBvh) : mode == kScanF32 ? RTW_PFN(false, kScanF32) : RTW_PFN(false, kScanF64);
         }
 #undef RTW_PFN
         int per_cu = 0;
