@@ -843,18 +843,48 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     ps.k = q.k;
     ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
     const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
+    // scenes of up to kCoopRegRec * kG spheres: the lane's pass-1 records live in
+    // registers for the whole pixel (no LDS round trip on the serial chain)
+    constexpr uint32_t kCoopRegRec = 8;
+    const bool rec_in_regs = n <= kCoopRegRec * kG;
+    float4 rr[kCoopRegRec];
+    if (rec_in_regs) {
+#pragma unroll
+        for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u)];
+    }
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                    double &bt) -> int {
         const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
         int best = -1;
         bt = 0.;
+        STAMP(0);  // coop: loop back + segment setup (Seg32)
+        if (rec_in_regs) {
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < kCoopRegRec; ++j) {
+                const uint32_t i = sub + j * kG;
+                mask |= static_cast<uint32_t>((i < n) & (!g.fast | g.pass(rr[j]))) << j;
+            }
+            STAMP(5);
+            while (mask) {
+                const uint32_t j = static_cast<uint32_t>(__builtin_ctz(mask));
+                mask &= mask - 1u;
+                ++tl.ntest;
+                exact_test(sph, sub + j * kG, ox, oy, oz, dx, dy, dz, a, best, bt);
+            }
+            STAMP(2);
+            group_min<kG>(bt, best);
+            return best;
+        }
         for (uint32_t base = 0; base < n; base += 32u * kG) {
             uint32_t mask = 0;  // bit j: sphere base + sub + j*kG is a candidate
             const uint32_t jn = min(32u, (n - base + kG - 1u) / kG);  // group-uniform
+            // branch-free: every load is issued before the first test needs it
 #pragma unroll 8
             for (uint32_t j = 0; j < jn; ++j) {
                 const uint32_t i = base + sub + j * kG;
-                if (i < n && (!g.fast || g.pass(filt[i]))) mask |= 1u << j;
+                const float4 rec = filt[min(i, n - 1u)];
+                mask |= static_cast<uint32_t>((i < n) & (!g.fast | g.pass(rec))) << j;
             }
             STAMP(5);  // coop: segment setup + filter
             while (mask) {

@@ -2,9 +2,9 @@
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp PYTHONPATH=.
-OUT=gpurun_out/pmc_${TAG:-bvh}
+OUT=gpurun_out/pmc_${TAG:-bvh}; CMD=${CMD:-"bench.py --steps 1 --warmup 0 --cpu-baseline 0"}
 mkdir -p $OUT
-run() { timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT/p$N -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 > $OUT/p$N.log 2>&1; N=$((N+1)); }
+run() { timeout -k 10 300 rocprofv3 --pmc "$@" -d $OUT/p$N -o run --output-format csv -- python3 $CMD > $OUT/p$N.log 2>&1; N=$((N+1)); }
 N=1
 run SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 run SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE
