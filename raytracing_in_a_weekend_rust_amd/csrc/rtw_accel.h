@@ -124,7 +124,10 @@ struct WalkRay {
     float ox, oy, oz;   // o32
     float ex, ey, ez;   // e32 (filter direction, ~unit)
     float ix, iy, iz;   // 1 / clamped e32
-    float alx, aly, alz, ahx, ahy, ahz;  // -(o -/+ pad) * inv: slab offsets, padded outward
+    // slab offsets, padded outward: t = plane * inv + a. The near plane of axis k
+    // is lo (q[2k]) for a non-negative direction, hi (q[2k+1]) for a negative one;
+    // an* go with the near plane, af* with the far plane.
+    float anx, any, anz, afx, afy, afz;
     float tmin;         // 0.01 |d| rounded down (distance units)
     float negG;         // -(filter margin G)
     uint32_t neg;       // bit k: e32 component k < 0 (near child = right on that axis)
@@ -145,9 +148,16 @@ RTW_HD bool walk_setup(float ox, float oy, float oz, float ex, float ey, float e
     r.neg = (ex < 0.f ? 1u : 0u) | (ey < 0.f ? 2u : 0u) | (ez < 0.f ? 4u : 0u);
     r.ix = rcp32(clamp_dir(ex)), r.iy = rcp32(clamp_dir(ey)), r.iz = rcp32(clamp_dir(ez));
     const float pad = kPadK * static_cast<float>(mo) + 1e-30f;
-    r.alx = -(ox + pad) * r.ix, r.ahx = -(ox - pad) * r.ix;
-    r.aly = -(oy + pad) * r.iy, r.ahy = -(oy - pad) * r.iy;
-    r.alz = -(oz + pad) * r.iz, r.ahz = -(oz - pad) * r.iz;
+    // lo-plane offset -(o + pad) inv, hi-plane offset -(o - pad) inv; for a
+    // negative direction the hi plane is the near one (same t values as testing
+    // both planes and taking min / max: the order is fixed by the sign of inv)
+    const float alx = -(ox + pad) * r.ix, ahx = -(ox - pad) * r.ix;
+    const float aly = -(oy + pad) * r.iy, ahy = -(oy - pad) * r.iy;
+    const float alz = -(oz + pad) * r.iz, ahz = -(oz - pad) * r.iz;
+    const bool nx = r.neg & 1u, ny = r.neg & 2u, nz = r.neg & 4u;
+    r.anx = nx ? ahx : alx, r.afx = nx ? alx : ahx;
+    r.any = ny ? ahy : aly, r.afy = ny ? aly : ahy;
+    r.anz = nz ? ahz : alz, r.afz = nz ? alz : ahz;
     r.tmin = static_cast<float>(0.01 * sa * (1. - 1e-6));
     r.negG = negG;
     return true;
@@ -171,16 +181,15 @@ RTW_HD float sqrt32(float x) {
 #endif
 }
 
-// One box slab test against the padded box of slot j (near distance out).
-template <typename F4>
-RTW_HD bool slab_hit(float lox, float hix, float loy, float hiy, float loz, float hiz,
-                     const WalkRay &r, float U) {
-    const float t0x = fmaf(lox, r.ix, r.alx), t1x = fmaf(hix, r.ix, r.ahx);
-    const float t0y = fmaf(loy, r.iy, r.aly), t1y = fmaf(hiy, r.iy, r.ahy);
-    const float t0z = fmaf(loz, r.iz, r.alz), t1z = fmaf(hiz, r.iz, r.ahz);
-    const float nr = fmax3(fminf(t0x, t1x), fminf(t0y, t1y), fminf(t0z, t1z));
-    const float fr = fmin3(fmaxf(t0x, t1x), fmaxf(t0y, t1y), fmaxf(t0z, t1z));
-    return !(nr > fr) && !(fr < r.tmin) && !(nr > U);
+// One box slab test against the padded box of a child: its near planes (nx, ny,
+// nz) and far planes (fx, fy, fz) for this ray's direction signs. Hit iff the
+// entry/exit interval meets [tmin, U] (all values finite: walk_setup rejects
+// non-finite rays, empty slots are masked by the caller).
+RTW_HD bool slab_hit(float nx, float ny, float nz, float fx, float fy, float fz, const WalkRay &r,
+                     float U) {
+    const float tn = fmax3(fmaf(nx, r.ix, r.anx), fmaf(ny, r.iy, r.any), fmaf(nz, r.iz, r.anz));
+    const float tf = fmin3(fmaf(fx, r.ix, r.afx), fmaf(fy, r.iy, r.afy), fmaf(fz, r.iz, r.afz));
+    return fmaxf(tn, r.tmin) <= fminf(tf, U);
 }
 
 // The pass-1 filter on leaf k; a kept sphere joins the candidate list (false on
@@ -276,6 +285,7 @@ template <typename F4, typename Stack>
 RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
                  float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits, Stack &stk) {
     uint32_t cur = 0;
+    const uint32_t sx = r.neg & 1u, sy = (r.neg >> 1) & 1u, sz = r.neg >> 2;
     const uint32_t oct_shift = 8u * (r.neg & 3u);
     const bool oct_hi = r.neg >= 4u;
     for (;;) {
@@ -285,12 +295,14 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         if (__builtin_ctzll(__builtin_amdgcn_read_exec()) == static_cast<int>(__lane_id())) visits += 1u << 16;
 #endif
         const F4 *N = nodes + kNodeF4 * cur;
-        const F4 qlx = N[0], qhx = N[1], qly = N[2], qhy = N[3], qlz = N[4], qhz = N[5], qc = N[6], qo = N[7];
+        // near / far planes picked by address (per-ray direction signs): no min/max
+        const F4 nX = N[sx], fX = N[sx ^ 1u], nY = N[2u + sy], fY = N[3u - sy], nZ = N[4u + sz],
+                 fZ = N[5u - sz], qc = N[6], qo = N[7];
         uint32_t hit = 0;
-        hit |= slab_hit<F4>(qlx.x, qhx.x, qly.x, qhy.x, qlz.x, qhz.x, r, U) ? 1u : 0u;
-        hit |= slab_hit<F4>(qlx.y, qhx.y, qly.y, qhy.y, qlz.y, qhz.y, r, U) ? 2u : 0u;
-        hit |= slab_hit<F4>(qlx.z, qhx.z, qly.z, qhy.z, qlz.z, qhz.z, r, U) ? 4u : 0u;
-        hit |= slab_hit<F4>(qlx.w, qhx.w, qly.w, qhy.w, qlz.w, qhz.w, r, U) ? 8u : 0u;
+        hit |= slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, U) ? 1u : 0u;
+        hit |= slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, U) ? 2u : 0u;
+        hit |= slab_hit(nX.z, nY.z, nZ.z, fX.z, fY.z, fZ.z, r, U) ? 4u : 0u;
+        hit |= slab_hit(nX.w, nY.w, nZ.w, fX.w, fY.w, fZ.w, r, U) ? 8u : 0u;
         const uint32_t r01 = as_u32(qc.x), r23 = as_u32(qc.y), masks = as_u32(qc.z);
         hit &= masks;
         // leaf children first: they may tighten U for the inner children
