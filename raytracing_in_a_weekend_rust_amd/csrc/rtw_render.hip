@@ -51,6 +51,7 @@ constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
 constexpr int kCounters = 8;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
+constexpr uint32_t kTailSegs = 768;     // dry-cursor parking: estimated segments left (RTW_TAIL)
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 
@@ -109,6 +110,7 @@ struct KParams {
     uint32_t n_node, n_leaf, n_always, seg_budget;
     uint32_t order, heavy_per_block;
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
+    uint32_t tail_segs, _pad5;  // once the cursor is dry: park pixels with more estimated work left
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
@@ -130,7 +132,9 @@ struct KParams {
     U128 *seeds;                // per-pixel RNG children (persistent phase 1)
     uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
     uint32_t *order_map;        // hand-out order of the persistent kernel (pixel per ticket) or null
-    uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base
+    uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base;
+                                // then per tile: its hot pixels
+    uint32_t *pcost;            // per pixel: probe segments
     uint32_t *cost_hist;        // [kCostBuckets] counts, then bucket write cursors
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
@@ -924,24 +928,32 @@ __device__ __forceinline__ const float4 *stage_filt(const KParams &P, float4 *lf
 
 // Hand-out order by estimated cost. rtw_cost_probe traces kProbeSamples of every
 // pixel's lattice (spread over the lattice) on a COPY of the pixel's RNG -- the
-// render itself is untouched -- and adds the segment count to the cost of the
-// pixel's 8x8 tile. Tiles are then bucketed by cost per sample (descending) and
-// laid out tile by tile (row-major inside a tile) in the order the persistent
-// kernel hands pixels out: expensive tiles start first, the cheapest fill the
-// drain, and lanes refilled together get neighbouring pixels (coherent rays).
+// render itself is untouched -- and records the pixel's segment count. "Hot"
+// pixels (>= kHotSegs probe segments: long serial chains) are ordered one by one
+// by their own cost; the others by the cost of their 8x8 tile. Units are
+// bucketed by cost per sample (descending) and laid out in the order the
+// persistent kernel hands pixels out: hot pixels and expensive tiles start first
+// (a chain started late ends late), the cheapest tiles fill the drain, and lanes
+// refilled together get neighbouring pixels (coherent rays).
 constexpr uint32_t kProbeSamples = 2;
+constexpr uint32_t kHotSegs = 2 * 10;  // probe segments: >= 10 per sample
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kOrderTile = 8;
 struct TileGrid {
     uint32_t tx, ty;
     __host__ __device__ TileGrid(const KParams &P)
         : tx((P.W + kOrderTile - 1) / kOrderTile), ty((P.n_rows + kOrderTile - 1) / kOrderTile) {}
+    __host__ __device__ uint32_t count() const { return tx * ty; }
     __device__ uint32_t of(uint32_t x, uint32_t lr) const { return (lr / kOrderTile) * tx + x / kOrderTile; }
     __device__ uint32_t pixels(const KParams &P, uint32_t t) const {
         const uint32_t bx = (t % tx) * kOrderTile, by = (t / tx) * kOrderTile;
         return min(kOrderTile, P.W - bx) * min(kOrderTile, P.n_rows - by);
     }
 };
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t segs, uint32_t pixels) {
+    const uint32_t per = static_cast<uint32_t>((8ull * segs) / (static_cast<uint64_t>(pixels) * kProbeSamples));
+    return kCostBuckets - 1u - min(per, kCostBuckets - 1u);  // 1/8 segment per sample
+}
 template <bool kLds>
 __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
@@ -969,19 +981,27 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
                 shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb);
             }
         }
-        atomicAdd(P.cost + TileGrid(P).of(x, lr), segs);
+        P.pcost[i] = segs;
+        const TileGrid tg(P);
+        if (segs >= kHotSegs) atomicAdd(P.cost + tg.count() + tg.of(x, lr), 1u);
+        else atomicAdd(P.cost + tg.of(x, lr), segs);
     }
 }
-// per tile: cost bucket (descending cost per sample) and its pixel count into the histogram
+// per tile: cost bucket of its non-hot pixels and their count into the histogram
 __global__ __launch_bounds__(kBlock) void rtw_cost_bucket(const KParams P) {
     const TileGrid tg(P);
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= tg.tx * tg.ty) return;
-    const uint32_t np = tg.pixels(P, t);
-    const uint32_t per = static_cast<uint32_t>((8ull * P.cost[t]) / (np * kProbeSamples));  // 1/8 seg/sample
-    const uint32_t b = kCostBuckets - 1u - min(per, kCostBuckets - 1u);
+    if (t >= tg.count()) return;
+    const uint32_t np = tg.pixels(P, t) - P.cost[tg.count() + t];
+    const uint32_t b = np ? cost_bucket(P.cost[t], np) : 0u;
     P.cost[t] = b;
-    atomicAdd(P.cost_hist + b, np);
+    if (np) atomicAdd(P.cost_hist + b, np);
+}
+// per hot pixel: its own bucket into the histogram
+__global__ __launch_bounds__(kBlock) void rtw_cost_hot_bucket(const KParams P) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
+    atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u);
 }
 // exclusive prefix sums of pixel counts over the buckets -> bucket write cursors
 __global__ void rtw_cost_scan(const KParams P) {
@@ -994,22 +1014,33 @@ __global__ void rtw_cost_scan(const KParams P) {
         }
     }
 }
-// per tile: its base in the order (tiles of one bucket in any order)
+// per tile: the base of its non-hot pixels in the order (tiles of one bucket in any order)
 __global__ __launch_bounds__(kBlock) void rtw_cost_place(const KParams P) {
     const TileGrid tg(P);
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= tg.tx * tg.ty) return;
-    P.cost[t] = atomicAdd(P.cost_hist + P.cost[t], tg.pixels(P, t));
+    if (t >= tg.count()) return;
+    const uint32_t np = tg.pixels(P, t) - P.cost[tg.count() + t];
+    if (np) P.cost[t] = atomicAdd(P.cost_hist + P.cost[t], np);
 }
-// per pixel: order[tile base + row-major rank inside the tile] = pixel
+// per hot pixel: its slot in the order
+__global__ __launch_bounds__(kBlock) void rtw_cost_hot_place(const KParams P) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
+    P.order_map[atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u)] = static_cast<uint32_t>(i);
+}
+// one wave per tile (lane = row-major rank in the tile): order[tile base + rank
+// among the tile's non-hot pixels] = pixel
 __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
     const TileGrid tg(P);
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= static_cast<uint64_t>(P.n_rows) * P.W) return;
-    const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
-    const uint32_t bx = (x / kOrderTile) * kOrderTile, wx = min(kOrderTile, P.W - bx);
-    const uint32_t rank = (lr % kOrderTile) * wx + (x - bx);
-    P.order_map[P.cost[tg.of(x, lr)] + rank] = static_cast<uint32_t>(i);
+    const uint32_t t = (blockIdx.x * kBlock + threadIdx.x) / 64u, r = threadIdx.x & 63u;
+    if (t >= tg.count()) return;  // wave-uniform
+    const uint32_t bx = (t % tg.tx) * kOrderTile, by = (t / tg.tx) * kOrderTile;
+    const uint32_t wx = min(kOrderTile, P.W - bx), wy = min(kOrderTile, P.n_rows - by);
+    const uint32_t x = bx + r % wx, lr = by + r / wx;
+    const uint64_t i = static_cast<uint64_t>(lr) * P.W + x;
+    const bool mine = r < wx * wy && P.pcost[i] < kHotSegs;
+    const uint64_t m = __ballot(mine);
+    if (mine) P.order_map[P.cost[t] + static_cast<uint32_t>(__popcll(m & ((1ull << r) - 1ull)))] = static_cast<uint32_t>(i);
 }
 
 // Phase 1, persistent form, with the heavy tail folded in. Every lane of a
@@ -1114,6 +1145,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
             }
             dry = dry || __any(dry_now);  // wave-uniform
+
             if (__all(need)) {
                 if (dry) break;
                 continue;
@@ -1128,7 +1160,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
                 acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 const bool done = ++ps.k >= P.n_off;
-                const bool park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k));
+                // park: the budget is spent, the rate runs away, or -- once the
+                // cursor is dry, so drain groups are about to be plentiful -- the
+                // estimated remaining work exceeds P.tail_segs
+                const bool park =
+                    !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
+                              (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
                 if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
                     atomicAdd(P.diag + 2 * pix, pseg);
                     __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
@@ -1277,6 +1314,7 @@ struct rtw_session {
     U128 *d_seeds = nullptr;         // per-pixel RNG children of the current shard
     uint32_t *d_park_flag = nullptr; // per park slot publish flags
     uint32_t *d_order = nullptr, *d_cost = nullptr, *d_cost_hist = nullptr;  // cost-ordered hand-out
+    uint32_t *d_pcost = nullptr;
     uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
     size_t diag_bytes = 0, diag_n = 0;
     int n_cu = 0;
@@ -1495,12 +1533,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         dev_free(s->d_park);
         s->d_park = nullptr, s->park_cap = 0;
         dev_free(s->d_seeds), dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost);
+        dev_free(s->d_pcost);
         s->d_seeds = nullptr, s->d_park_flag = nullptr, s->d_order = nullptr, s->d_cost = nullptr;
+        s->d_pcost = nullptr;
         HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
         HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
         HIPCHECK(hipMalloc(&s->d_park_flag, npix_sh * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_order, npix_sh * sizeof(uint32_t)));
-        HIPCHECK(hipMalloc(&s->d_cost, npix_sh * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_cost, 2 * npix_sh * sizeof(uint32_t)));  // 2 words per 8x8 tile
+        HIPCHECK(hipMalloc(&s->d_pcost, npix_sh * sizeof(uint32_t)));
         s->park_cap = npix_sh;
     }
     P.park = s->d_park;
@@ -1586,19 +1627,22 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // bottom-up, 0 row-major
         P.order_map = nullptr;
         if (P.order == 2 && mode == kBvh && P.max_depth > 0) {
-            P.cost = s->d_cost, P.cost_hist = s->d_cost_hist, P.order_map = s->d_order;
+            P.cost = s->d_cost, P.cost_hist = s->d_cost_hist, P.order_map = s->d_order, P.pcost = s->d_pcost;
             const dim3 g1(static_cast<uint32_t>((npix + kBlock - 1) / kBlock));
             const TileGrid tg(P);
-            const dim3 gt((tg.tx * tg.ty + kBlock - 1) / kBlock);
+            const dim3 gt((tg.count() + kBlock - 1) / kBlock);
+            const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
-            HIPCHECK(hipMemsetAsync(s->d_cost, 0, static_cast<size_t>(tg.tx) * tg.ty * sizeof(uint32_t), st));
+            HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
             const size_t lds_p = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true);
             if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, g1, dim3(kBlock), lds_p, st, P);
             else hipLaunchKernelGGL(rtw_cost_probe<false>, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_bucket, gt, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_hot_bucket, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_scan, dim3(1), dim3(64), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_place, gt, dim3(kBlock), 0, st, P);
-            hipLaunchKernelGGL(rtw_cost_scatter, g1, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_hot_place, g1, dim3(kBlock), 0, st, P);
+            hipLaunchKernelGGL(rtw_cost_scatter, gw, dim3(kBlock), 0, st, P);
             HIPCHECK(hipGetLastError());
         }
         const int pblock = kPBlock;
@@ -1633,6 +1677,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         P.heavy_per_block = heavy;
         P.n_cursor_waves = grid_p * (wpb - heavy);
         P.rate_k = 16, P.rate_x = 16;
+        P.tail_segs = kTailSegs;
+        if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
@@ -1777,6 +1823,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
+    dev_free(s->d_pcost);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);

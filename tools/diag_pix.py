@@ -41,3 +41,9 @@ bins = np.arange(0, done.max() + 10, 10)
 h, _ = np.histogram(t[ran], bins=bins, weights=cost[ran])
 print("segments completed per 10 ms (M):", [round(float(v) / 1e6, 1) for v in h])
 sess.close()
+last = np.argsort(-np.where(ran, t, -1))[:12]
+print("last finishers (x, y, seg/sample, done ms):",
+      [(int(i % W), int(i // W), round(float(seg[i]), 1), round(float(t[i]), 1)) for i in last])
+late = ran & (t > np.percentile(done, 99.9))
+print(f"pixels done after the 99.9% mark: {int(late.sum())}, their seg/sample: "
+      f"p50 {np.percentile(seg[late], 50):.1f} max {seg[late].max():.1f}")
