@@ -49,7 +49,7 @@ constexpr double kPadKd = 1.52587890625e-05;
 constexpr float kDirFloor = 9.094947017729282e-13f;  // 2^-40: |e_i| clamp before 1/e_i
 constexpr float kGuardBvh = 1e8f;       // |origin| beyond -> brute force for the segment
 constexpr uint32_t kMaxSpheres = 32768;  // 16-bit leaf / node ids
-constexpr uint32_t kStack = 16;          // register stack: 4 x u64 of 16-bit entries
+constexpr uint32_t kStack = 16;          // traversal stack entries (16-bit node ids)
 constexpr uint32_t kEmpty = 0xffffffffu;  // "no node"
 // Node stride 9 float4 (144 B): with 8 (128 B) every node starts on one of 2 of
 // the 16 four-bank slots and ds_read_b128 gathers of different nodes conflict
@@ -219,56 +219,40 @@ RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     return true;
 }
 
-// Traversal stacks of 16-bit node ids (LIFO, kStack entries). push(L, m): the
-// m entries packed in L (16 bits each, bits 0.. nearest) go on top so that the
-// nearest is popped first.
-// RegStack: 4 x u64 in registers, a push of m entries is one variable shift.
-struct RegStack {
-    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+// Traversal stacks of 16-bit node ids (LIFO). put(id, h) stores id on top and
+// keeps it iff h (a write that is not kept is overwritten by the next put):
+// the walk puts every child slot far to near without branching. Up to
+// kStackSlots entries are written; more than kStack kept is an overflow.
+constexpr uint32_t kStackSlots = kStack + 4;
+// ArrayStack (host, accel_check): a plain array.
+struct ArrayStack {
+    uint16_t e[kStackSlots] = {};
     uint32_t sp = 0;
-    RTW_HD bool push(uint64_t L, uint32_t m) {
-        if (sp + m > kStack) return false;
-        const uint32_t sh = 16u * m;  // 0..48
-        s3 = (s3 << sh) | ((s2 >> 1) >> (63u - sh));
-        s2 = (s2 << sh) | ((s1 >> 1) >> (63u - sh));
-        s1 = (s1 << sh) | ((s0 >> 1) >> (63u - sh));
-        s0 = (s0 << sh) | L;
-        sp += m;
-        return true;
+    RTW_HD void put(uint32_t id, uint32_t h) {
+        if (sp < kStackSlots) e[sp] = static_cast<uint16_t>(id);
+        sp += h;
     }
+    RTW_HD bool overflow() const { return sp > kStack; }
     RTW_HD bool pop(uint32_t &next) {
         if (sp == 0) return false;
-        next = static_cast<uint32_t>(s0 & 0xffffu);
-        s0 = (s0 >> 16) | (s1 << 48);
-        s1 = (s1 >> 16) | (s2 << 48);
-        s2 = (s2 >> 16) | (s3 << 48);
-        s3 >>= 16;
-        --sp;
+        next = e[--sp];
         return true;
     }
 };
 #if defined(__HIPCC__)
-// LdsStack (device): the top entry in a register, the rest in a per-lane LDS
-// column (entry k at col[k * stride], u16). A pop hands out the register and
-// reloads it from LDS -- the load completes while the next node is tested.
+// LdsStack (device): a per-lane LDS column, entry k at col[k * stride] (u16).
 struct LdsStack {
     uint16_t *col;
-    uint32_t stride, n = 0, top = 0;  // n: entries in LDS; top valid iff sp > 0
-    uint32_t sp = 0;
+    uint32_t stride, sp = 0;
     __device__ LdsStack(uint16_t *c, uint32_t s) : col(c), stride(s) {}
-    __device__ bool push(uint64_t L, uint32_t m) {
-        if (sp + m > kStack) return false;
-        if (m == 0) return true;
-        if (sp) col[n++ * stride] = static_cast<uint16_t>(top);
-        for (uint32_t i = m - 1u; i > 0; --i) col[n++ * stride] = static_cast<uint16_t>(L >> (16u * i));
-        top = static_cast<uint32_t>(L & 0xffffu);
-        sp += m;
-        return true;
+    __device__ void put(uint32_t id, uint32_t h) {
+        col[sp * stride] = static_cast<uint16_t>(id);
+        sp += h;
     }
+    __device__ bool overflow() const { return sp > kStack; }
     __device__ bool pop(uint32_t &next) {
         if (sp == 0) return false;
-        next = top;
-        if (--sp) top = col[--n * stride];
+        next = col[--sp * stride];
         return true;
     }
 };
@@ -277,7 +261,7 @@ struct LdsStack {
 // Collects the leaves (leaf-order ids) the walk cannot rule out. Each iteration
 // takes one 4-wide node, tests its 4 child boxes, runs the leaf filter on hit
 // leaf children, continues with the nearest hit inner child and pushes the
-// other hit inner children (k - 1 at a time). U (distance units along e32) is
+// other hit inner children. U (distance units along e32) is
 // the running cut; the caller seeds it from the "always" spheres. Returns false
 // on candidate-list or stack overflow (caller brute-forces). `visits` counts
 // loop iterations (node visits).
@@ -314,23 +298,15 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
             const uint32_t k = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
             if (!leaf_test(leaves, k, r, U, c0, c1, nc)) return false;
         }
-        // hit inner children packed near to far: L (16 bits each), count nk
+        // hit inner children onto the stack far to near (branch-free puts), then
+        // continue with the top = the nearest
         const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
-        uint64_t L = 0;
-        uint32_t nk = 0;
-        for (uint32_t t = 0; t < 4; ++t) {
-            const uint32_t j = (ord >> (2u * t)) & 3u;
-            const uint32_t id = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
-            const uint32_t h = (inner >> j) & 1u;
-            L |= static_cast<uint64_t>(h ? id : 0u) << (16u * nk);
-            nk += h;
+        for (int t = 3; t >= 0; --t) {
+            const uint32_t j = (ord >> (2 * t)) & 3u;
+            stk.put(((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu, (inner >> j) & 1u);
         }
-        if (nk) {  // continue with the nearest, push the other nk - 1
-            if (!stk.push(L >> 16, nk - 1u)) return false;
-            cur = static_cast<uint32_t>(L & 0xffffu);
-        } else if (!stk.pop(cur)) {
-            break;
-        }
+        if (stk.overflow()) return false;
+        if (!stk.pop(cur)) break;
     }
     return true;
 }

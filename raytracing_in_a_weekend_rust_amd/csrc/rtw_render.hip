@@ -160,14 +160,26 @@ __device__ __forceinline__ void xs_step(U128 &s) {
 // random.rs:40-52: u128 % (2^32-1) by limb folding (2^32 == 1 mod 2^32-1),
 // then m / 4294967295.0 correctly rounded, computed division-free
 // (rtw_numeric.h; exhaustively equal to the IEEE divide for every m).
-__device__ __forceinline__ double xs_next_01(U128 &s) {
+__device__ __forceinline__ uint32_t xs_next_m(U128 &s) {
     xs_step(s);
     uint64_t t = (s.lo & 0xffffffffull) + (s.lo >> 32) + (s.hi & 0xffffffffull) + (s.hi >> 32);
     t = (t & 0xffffffffull) + (t >> 32);
     t = (t & 0xffffffffull) + (t >> 32);
-    const uint32_t m = t == 0xffffffffull ? 0u : static_cast<uint32_t>(t);
-    return rtw_num::next01_of(m);
+    return t == 0xffffffffull ? 0u : static_cast<uint32_t>(t);
 }
+__device__ __forceinline__ double xs_next_01(U128 &s) { return rtw_num::next01_of(xs_next_m(s)); }
+
+// Rejection sampling on -1 + 2 next_01(): the candidate is first judged in f32
+// from the raw draws m. |x32 - x64| <= 2^-22.5 per coordinate (f32 conversion,
+// the m / (2^32 - 1) vs m 2^-32 scale, roundings), so a squared length within
+// 2^-17 of 1 is the only case that needs the exact f64 value; accepted
+// candidates are then rebuilt exactly. (Same draws, same decisions as the f64
+// loop: the RNG advances identically.)
+constexpr float kRejBand = 7.62939453125e-06f;  // 2^-17
+__device__ __forceinline__ float coord32(uint32_t m) {
+    return fmaf(static_cast<float>(m), 4.656612873077393e-10f, -1.f);  // 2 m 2^-32 - 1
+}
+__device__ __forceinline__ double coord64(uint32_t m) { return -1. + rtw_num::next01_of(m) * 2.; }
 // random.rs:61-69: the child handed out by copy_reset at parent state p
 __device__ __forceinline__ U128 child_of(U128 p) {
     U128 n = p;
@@ -213,12 +225,15 @@ __device__ __forceinline__ U128 jump_state(U128 s, uint64_t p, const uint4 *__re
 // vec3.rs:207-232: rejection in [-1,1]^3 with len^2 <= 1, then / sqrt(len^2)
 __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &uy, double &uz) {
     double x, y, z, l2;
-    do {
-        x = -1. + xs_next_01(rng) * 2.;
-        y = -1. + xs_next_01(rng) * 2.;
-        z = -1. + xs_next_01(rng) * 2.;
+    for (;;) {
+        const uint32_t m0 = xs_next_m(rng), m1 = xs_next_m(rng), m2 = xs_next_m(rng);
+        const float x32 = coord32(m0), y32 = coord32(m1), z32 = coord32(m2);
+        const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
+        if (l32 > 1.f + kRejBand) continue;  // surely rejected
+        x = coord64(m0), y = coord64(m1), z = coord64(m2);
         l2 = x * x + y * y + z * z;
-    } while (!(l2 <= 1.));
+        if (l32 < 1.f - kRejBand || l2 <= 1.) break;  // surely / exactly accepted
+    }
     const double l = __builtin_sqrt(l2);
     ux = x / l;
     uy = y / l;
@@ -310,9 +325,9 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
            (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
 }
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
-// sum (3 x f64 columns) and the BVH walk stack (kStack x u16 columns).
+// sum (3 x f64 columns) and the BVH walk stack (kStackSlots x u16 columns).
 __host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
-    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kStack * sizeof(uint16_t));
+    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kStackSlots * sizeof(uint16_t));
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -353,10 +368,15 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
         p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
     } else {
         double px, py;
-        do {  // vec3.rs:270-277: strict len^2 < 1
-            px = -1. + 2. * xs_next_01(rng);
-            py = -1. + 2. * xs_next_01(rng);
-        } while (!((px * px + py * py + 0. * 0.) < 1.));
+        for (;;) {  // vec3.rs:270-277: strict len^2 < 1 (f32 pre-judged, as random_unit_vec)
+            const uint32_t m0 = xs_next_m(rng), m1 = xs_next_m(rng);
+            const float x32 = coord32(m0), y32 = coord32(m1);
+            const float l32 = fmaf(x32, x32, y32 * y32);
+            if (l32 > 1.f + kRejBand) continue;
+            px = -1. + 2. * rtw_num::next01_of(m0);
+            py = -1. + 2. * rtw_num::next01_of(m1);
+            if (l32 < 1.f - kRejBand || (px * px + py * py + 0. * 0.) < 1.) break;
+        }
         p.ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
         p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
         p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
@@ -633,7 +653,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
                 rtw_accel::LdsStack stk(scol, blockDim.x);
                 walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
             } else {
-                rtw_accel::RegStack stk;
+                rtw_accel::ArrayStack stk;
                 walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
             }
             STAMP(2);  // 2: BVH walk
@@ -1064,7 +1084,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf;
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
     // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
-    // read and written once per sample) and the BVH walk stack (kStack u16
+    // read and written once per sample) and the BVH walk stack (kStackSlots u16
     // columns) -- state that would otherwise hold ~12 VGPRs through the walk
     double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
     uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);

@@ -98,7 +98,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
     if (h.idx >= 0) U = seed_cut(h.t, sa);
     uint64_t c0 = 0, c1 = 0;
     uint32_t nc = 0, visits = 0;
-    RegStack stk;
+    ArrayStack stk;
     const bool ok = walk(reinterpret_cast<const F4 *>(S.bvh.nodes.data()),
                          reinterpret_cast<const F4 *>(S.bvh.leaves.data()), wr, U, c0, c1, nc, visits, stk);
     k.visits += visits;
