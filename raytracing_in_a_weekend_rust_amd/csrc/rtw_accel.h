@@ -49,7 +49,6 @@ constexpr double kPadKd = 1.52587890625e-05;
 constexpr float kDirFloor = 9.094947017729282e-13f;  // 2^-40: |e_i| clamp before 1/e_i
 constexpr float kGuardBvh = 1e8f;       // |origin| beyond -> brute force for the segment
 constexpr uint32_t kMaxSpheres = 32768;  // 16-bit leaf / node ids
-constexpr uint32_t kStack = 16;          // traversal stack entries (16-bit node ids)
 constexpr uint32_t kEmpty = 0xffffffffu;  // "no node"
 // Node stride 9 float4 (144 B): with 8 (128 B) every node starts on one of 2 of
 // the 16 four-bank slots and ds_read_b128 gathers of different nodes conflict
@@ -57,7 +56,7 @@ constexpr uint32_t kEmpty = 0xffffffffu;  // "no node"
 constexpr uint32_t kNodeF4 = 9;
 constexpr uint32_t kNodeFloats = 4 * kNodeF4;
 constexpr uint32_t kMaxAlways = 16;
-constexpr uint32_t kMaxCand = 8;        // candidate list: 2 x u64 of 16-bit entries
+constexpr uint32_t kMaxCand = 8;        // candidate list entries (walk scratch)
 constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -> "always"
 
 // Node (128 B, eight float4; 4-wide, children in the parent):
@@ -195,19 +194,16 @@ RTW_HD bool slab_hit(float nx, float ny, float nz, float fx, float fy, float fz,
 // The pass-1 filter on leaf k; a kept sphere joins the candidate list (false on
 // overflow) and, if it is a sure hit (disc beyond the filter's inflation + error,
 // far root clearly past tmin), its far root bounds the closest hit: U shrinks.
-template <typename F4>
+template <typename F4, typename Scratch>
 RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &r, float &U,
-                      uint64_t &c0, uint64_t &c1, uint32_t &nc) {
+                      Scratch &ws) {
     const F4 S = leaves[2 * k];
     const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
     if (disc < r.negG) return true;
-    if (nc >= kMaxCand) return false;
-    if (nc < 4) c0 |= static_cast<uint64_t>(k) << (16u * nc);
-    else c1 |= static_cast<uint64_t>(k) << (16u * (nc - 4u));
-    ++nc;
+    if (!ws.add_cand(k)) return false;
     const float d2 = leaves[2 * k + 1].x;
     if (disc > d2 - 2.f * r.negG) {
         const float sd = sqrt32(disc);
@@ -219,42 +215,57 @@ RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     return true;
 }
 
-// Traversal stacks of 16-bit node ids (LIFO). put(id, h) stores id on top and
-// keeps it iff h (a write that is not kept is overwritten by the next put):
-// the walk puts every child slot far to near without branching. Up to
-// kStackSlots entries are written; more than kStack kept is an overflow.
-constexpr uint32_t kStackSlots = kStack + 4;
-// ArrayStack (host, accel_check): a plain array.
-struct ArrayStack {
-    uint16_t e[kStackSlots] = {};
-    uint32_t sp = 0;
+// Walk scratch: the traversal stack of 16-bit node ids (LIFO) and the candidate
+// list of leaf ids, sharing kScratch slots -- the stack grows up from slot 0,
+// the candidates down from the last slot. put(id, h) stores id on top and keeps
+// it iff h (a write that is not kept is overwritten by the next put): the walk
+// puts every child slot far to near without branching, so up to 4 slots above
+// the kept entries are written. Invariant: kept + 4 + candidates <= kScratch
+// (else overflow: the caller brute-forces), at most kMaxCand candidates.
+constexpr uint32_t kScratch = 24;
+// ArrayScratch (host, accel_check): a plain array.
+struct ArrayScratch {
+    uint16_t e[kScratch] = {};
+    uint32_t sp = 0, nc = 0;
     RTW_HD void put(uint32_t id, uint32_t h) {
-        if (sp < kStackSlots) e[sp] = static_cast<uint16_t>(id);
+        e[sp] = static_cast<uint16_t>(id);
         sp += h;
     }
-    RTW_HD bool overflow() const { return sp > kStack; }
+    RTW_HD bool overflow() const { return sp + 4u + nc > kScratch; }
     RTW_HD bool pop(uint32_t &next) {
         if (sp == 0) return false;
         next = e[--sp];
         return true;
     }
+    RTW_HD bool add_cand(uint32_t k) {
+        if (nc >= kMaxCand || sp + 5u + nc > kScratch) return false;
+        e[kScratch - 1u - nc++] = static_cast<uint16_t>(k);
+        return true;
+    }
+    RTW_HD uint32_t cand(uint32_t j) const { return e[kScratch - 1u - j]; }
 };
 #if defined(__HIPCC__)
-// LdsStack (device): a per-lane LDS column, entry k at col[k * stride] (u16).
-struct LdsStack {
+// LdsScratch (device): a per-lane LDS column, slot k at col[k * stride] (u16).
+struct LdsScratch {
     uint16_t *col;
-    uint32_t stride, sp = 0;
-    __device__ LdsStack(uint16_t *c, uint32_t s) : col(c), stride(s) {}
+    uint32_t stride, sp = 0, nc = 0;
+    __device__ LdsScratch(uint16_t *c, uint32_t s) : col(c), stride(s) {}
     __device__ void put(uint32_t id, uint32_t h) {
         col[sp * stride] = static_cast<uint16_t>(id);
         sp += h;
     }
-    __device__ bool overflow() const { return sp > kStack; }
+    __device__ bool overflow() const { return sp + 4u + nc > kScratch; }
     __device__ bool pop(uint32_t &next) {
         if (sp == 0) return false;
         next = col[--sp * stride];
         return true;
     }
+    __device__ bool add_cand(uint32_t k) {
+        if (nc >= kMaxCand || sp + 5u + nc > kScratch) return false;
+        col[(kScratch - 1u - nc++) * stride] = static_cast<uint16_t>(k);
+        return true;
+    }
+    __device__ uint32_t cand(uint32_t j) const { return col[(kScratch - 1u - j) * stride]; }
 };
 #endif
 
@@ -265,9 +276,9 @@ struct LdsStack {
 // the running cut; the caller seeds it from the "always" spheres. Returns false
 // on candidate-list or stack overflow (caller brute-forces). `visits` counts
 // loop iterations (node visits).
-template <typename F4, typename Stack>
+template <typename F4, typename Scratch>
 RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
-                 float &U, uint64_t &c0, uint64_t &c1, uint32_t &nc, uint32_t &visits, Stack &stk) {
+                 float &U, uint32_t &visits, Scratch &stk) {
     uint32_t cur = 0;
     const uint32_t sx = r.neg & 1u, sy = (r.neg >> 1) & 1u, sz = r.neg >> 2;
     const uint32_t oct_shift = 8u * (r.neg & 3u);
@@ -296,7 +307,7 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
             const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
             lmask &= lmask - 1u;
             const uint32_t k = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
-            if (!leaf_test(leaves, k, r, U, c0, c1, nc)) return false;
+            if (!leaf_test(leaves, k, r, U, stk)) return false;
         }
         // hit inner children onto the stack far to near (branch-free puts), then
         // continue with the top = the nearest
@@ -309,10 +320,6 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         if (!stk.pop(cur)) break;
     }
     return true;
-}
-
-RTW_HD uint32_t cand_at(uint64_t c0, uint64_t c1, uint32_t j) {
-    return static_cast<uint32_t>((j < 4 ? c0 >> (16u * j) : c1 >> (16u * (j - 4u))) & 0xffffu);
 }
 
 // (t, i) beats (bt, best) under the scan's first-minimum rule.

@@ -325,9 +325,9 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
            (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
 }
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
-// sum (3 x f64 columns) and the BVH walk stack (kStackSlots x u16 columns).
+// sum (3 x f64 columns) and the BVH walk scratch (kScratch x u16 columns).
 __host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
-    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kStackSlots * sizeof(uint16_t));
+    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t));
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -646,26 +646,28 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
             brute = true;
         } else {
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
-            uint64_t c0 = 0, c1 = 0;
-            uint32_t nc = 0;
+            auto run = [&](auto &ws) {
+                const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
+                STAMP(2);  // 2: BVH walk
+                if (!walked) return false;
+                for (uint32_t j = 0; j < ws.nc; ++j) {
+                    ++tl.ntest;
+                    exact_test(sph, __float_as_uint(leaves[2u * ws.cand(j) + 1u].y), ox, oy, oz, dx, dy, dz,
+                               a, best, bt);
+                }
+                return true;
+            };
             bool walked;
             if constexpr (kLdsStack) {
-                rtw_accel::LdsStack stk(scol, blockDim.x);
-                walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
+                rtw_accel::LdsScratch ws(scol, blockDim.x);
+                walked = run(ws);
             } else {
-                rtw_accel::ArrayStack stk;
-                walked = rtw_accel::walk(nodes, leaves, wr, U, c0, c1, nc, tl.visits, stk);
+                rtw_accel::ArrayScratch ws;
+                walked = run(ws);
             }
-            STAMP(2);  // 2: BVH walk
             if (!walked) {
                 brute = true;
             } else {
-                for (uint32_t j = 0; j < nc; ++j) {
-                    const uint32_t leaf = rtw_accel::cand_at(c0, c1, j);
-                    ++tl.ntest;
-                    exact_test(sph, __float_as_uint(leaves[2u * leaf + 1u].y), ox, oy, oz, dx, dy, dz,
-                               a, best, bt);
-                }
                 brute = !rtw_accel::cut_ok(U, best, bt, g.sa);
             }
         }
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf;
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
     // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
-    // read and written once per sample) and the BVH walk stack (kStackSlots u16
+    // read and written once per sample) and the BVH walk scratch (kScratch u16
     // columns) -- state that would otherwise hold ~12 VGPRs through the walk
     double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
     uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);

@@ -96,11 +96,11 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
     ++k.walked;
     float U = INFINITY;
     if (h.idx >= 0) U = seed_cut(h.t, sa);
-    uint64_t c0 = 0, c1 = 0;
-    uint32_t nc = 0, visits = 0;
-    ArrayStack stk;
+    uint32_t visits = 0;
+    ArrayScratch ws;
     const bool ok = walk(reinterpret_cast<const F4 *>(S.bvh.nodes.data()),
-                         reinterpret_cast<const F4 *>(S.bvh.leaves.data()), wr, U, c0, c1, nc, visits, stk);
+                         reinterpret_cast<const F4 *>(S.bvh.leaves.data()), wr, U, visits, ws);
+    const uint32_t nc = ws.nc;
     k.visits += visits;
     if (visits > k.max_visits) k.max_visits = visits;
     k.cands += nc;
@@ -109,7 +109,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
         return brute(S, o, d);
     }
     for (uint32_t j = 0; j < nc; ++j) {
-        const uint32_t leaf = cand_at(c0, c1, j);
+        const uint32_t leaf = ws.cand(j);
         const uint32_t i = as_u32(S.bvh.leaves[8 * leaf + 5]);
         double t;
         if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
