@@ -160,12 +160,17 @@ __device__ __forceinline__ void xs_step(U128 &s) {
 // random.rs:40-52: u128 % (2^32-1) by limb folding (2^32 == 1 mod 2^32-1),
 // then m / 4294967295.0 correctly rounded, computed division-free
 // (rtw_numeric.h; exhaustively equal to the IEEE divide for every m).
+// u128 mod (2^32-1) = the four 32-bit limbs summed mod 2^32-1 (2^32 == 1): a
+// 32-bit sum with its carries, the carries folded back in, 2^32-1 -> 0.
 __device__ __forceinline__ uint32_t xs_next_m(U128 &s) {
     xs_step(s);
-    uint64_t t = (s.lo & 0xffffffffull) + (s.lo >> 32) + (s.hi & 0xffffffffull) + (s.hi >> 32);
-    t = (t & 0xffffffffull) + (t >> 32);
-    t = (t & 0xffffffffull) + (t >> 32);
-    return t == 0xffffffffull ? 0u : static_cast<uint32_t>(t);
+    unsigned c0, c1, c2, c3;
+    uint32_t t = __builtin_addc(static_cast<uint32_t>(s.lo), static_cast<uint32_t>(s.lo >> 32), 0u, &c0);
+    t = __builtin_addc(t, static_cast<uint32_t>(s.hi), 0u, &c1);
+    t = __builtin_addc(t, static_cast<uint32_t>(s.hi >> 32), 0u, &c2);
+    t = __builtin_addc(t, c0 + c1 + c2, 0u, &c3);  // wraps at most once, to <= 2
+    t += c3;
+    return t == 0xffffffffu ? 0u : t;
 }
 __device__ __forceinline__ double xs_next_01(U128 &s) { return rtw_num::next01_of(xs_next_m(s)); }
 
