@@ -242,30 +242,36 @@ struct ArrayScratch {
         e[kScratch - 1u - nc++] = static_cast<uint16_t>(k);
         return true;
     }
-    RTW_HD uint32_t cand(uint32_t j) const { return e[kScratch - 1u - j]; }
+    RTW_HD uint32_t cand_at(uint32_t j) const { return e[kScratch - 1u - j]; }
 };
 #if defined(__HIPCC__)
-// LdsScratch (device): a per-lane LDS column, slot k at col[k * stride] (u16).
+// LdsScratch (device): a per-lane LDS column, slot k at col[k * stride] (u16);
+// kept as pointers (no multiplies on the walk): top = next stack slot, cand =
+// next candidate slot, lim = the highest top that keeps 4 free slots below cand.
 struct LdsScratch {
-    uint16_t *col;
-    uint32_t stride, sp = 0, nc = 0;
-    __device__ LdsScratch(uint16_t *c, uint32_t s) : col(c), stride(s) {}
+    uint16_t *base, *top, *cand, *lim;
+    uint32_t stride, nc = 0;
+    __device__ LdsScratch(uint16_t *c, uint32_t s)
+        : base(c), top(c), cand(c + (kScratch - 1u) * s), lim(c + (kScratch - 4u) * s), stride(s) {}
     __device__ void put(uint32_t id, uint32_t h) {
-        col[sp * stride] = static_cast<uint16_t>(id);
-        sp += h;
+        *top = static_cast<uint16_t>(id);
+        // h in {0, 1}: one v_mad_u32_u24 on the byte address
+        top = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(top) + __umul24(h, 2u * stride));
     }
-    __device__ bool overflow() const { return sp + 4u + nc > kScratch; }
+    __device__ bool overflow() const { return top > lim; }
     __device__ bool pop(uint32_t &next) {
-        if (sp == 0) return false;
-        next = col[--sp * stride];
+        if (top == base) return false;
+        top -= stride;
+        next = *top;
         return true;
     }
     __device__ bool add_cand(uint32_t k) {
-        if (nc >= kMaxCand || sp + 5u + nc > kScratch) return false;
-        col[(kScratch - 1u - nc++) * stride] = static_cast<uint16_t>(k);
+        if (nc >= kMaxCand || top >= lim) return false;
+        *cand = static_cast<uint16_t>(k);
+        cand -= stride, lim -= stride, ++nc;
         return true;
     }
-    __device__ uint32_t cand(uint32_t j) const { return col[(kScratch - 1u - j) * stride]; }
+    __device__ uint32_t cand_at(uint32_t j) const { return base[(kScratch - 1u - j) * stride]; }
 };
 #endif
 
@@ -312,9 +318,14 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         // hit inner children onto the stack far to near (branch-free puts), then
         // continue with the top = the nearest
         const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
+        const uint64_t refs = (static_cast<uint64_t>(r23) << 32) | r01;
         for (int t = 3; t >= 0; --t) {
             const uint32_t j = (ord >> (2 * t)) & 3u;
-            stk.put(((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu, (inner >> j) & 1u);
+#if defined(__HIP_DEVICE_COMPILE__)
+            stk.put(static_cast<uint32_t>(refs >> (16u * j)), __builtin_amdgcn_ubfe(inner, j, 1u));
+#else
+            stk.put(static_cast<uint32_t>(refs >> (16u * j)), (inner >> j) & 1u);
+#endif
         }
         if (stk.overflow()) return false;
         if (!stk.pop(cur)) break;

@@ -657,7 +657,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restri
                 if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
                     ++tl.ntest;
-                    exact_test(sph, __float_as_uint(leaves[2u * ws.cand(j) + 1u].y), ox, oy, oz, dx, dy, dz,
+                    exact_test(sph, __float_as_uint(leaves[2u * ws.cand_at(j) + 1u].y), ox, oy, oz, dx, dy, dz,
                                a, best, bt);
                 }
                 return true;

@@ -109,7 +109,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
         return brute(S, o, d);
     }
     for (uint32_t j = 0; j < nc; ++j) {
-        const uint32_t leaf = ws.cand(j);
+        const uint32_t leaf = ws.cand_at(j);
         const uint32_t i = as_u32(S.bvh.leaves[8 * leaf + 5]);
         double t;
         if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
