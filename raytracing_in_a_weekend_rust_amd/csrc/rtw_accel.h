@@ -295,7 +295,16 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         // diagnostic: wave-level iterations, counted by the first active lane in bit 16+
         if (__builtin_ctzll(__builtin_amdgcn_read_exec()) == static_cast<int>(__lane_id())) visits += 1u << 16;
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+        // byte offset by a full-rate v_mul_u32_u24 (ids < 2^16; the compiler
+        // otherwise picks the quarter-rate v_mul_lo_u32)
+        uint32_t off;
+        static_assert(kNodeF4 * 16u == 144u, "node stride");
+        asm("v_mul_u32_u24 %0, 0x90, %1" : "=v"(off) : "v"(cur));
+        const F4 *N = reinterpret_cast<const F4 *>(reinterpret_cast<const char *>(nodes) + off);
+#else
         const F4 *N = nodes + kNodeF4 * cur;
+#endif
         // near / far planes picked by address (per-ray direction signs): no min/max
         const F4 nX = N[sx], fX = N[sx ^ 1u], nY = N[2u + sy], fY = N[3u - sy], nZ = N[4u + sz],
                  fZ = N[5u - sz], qc = N[6], qo = N[7];
