@@ -1106,11 +1106,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
 
-    Stamps stp_unused;
+    Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true>(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp_unused,
+            return bvh_hit<true>(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp,
                                  lane_stk + threadIdx.x);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
@@ -1181,9 +1181,13 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             ++tl.seg, ++pseg;
             const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
             double bt = 0.;
+            STAMP(0);  // 0: loop top, refill
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+            STAMP(1);  // 1: hit tail (exact candidates, cut check)
             double cr, cg, cb;
-            if (shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb)) {
+            const bool ended = shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb);
+            STAMP(3);  // 3: hit record + scatter / sky
+            if (ended) {
                 fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
                 acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 const bool done = ++ps.k >= P.n_off;
@@ -1215,7 +1219,24 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, ps.rng, p);
                 }
             }
+            STAMP(4);  // 4: fold + next sample / pixel end
         }
+#ifdef RTW_STAMPS
+        {  // diagnostic: per cursor wave, the max over lanes of each section sum
+            uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.x) * (kThreads / 64u) + threadIdx.x / 64u) * 8;
+            for (int k = 0; k < 6; ++k) {
+                uint64_t v = stp.acc[k];
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v, off);
+                    v = v > o ? v : o;
+                }
+                if (lane == 0) row[k] = v;
+            }
+            uint32_t wi = tl.witer;  // wave iterations (counted on one lane each)
+            for (int off = 32; off > 0; off >>= 1) wi += static_cast<uint32_t>(__shfl_xor(static_cast<int>(wi), off));
+            if (lane == 0) row[6] = wi, row[7] = stamp_now();
+        }
+#endif
         // this wave parks no more (its parks are published: drained stores + flags)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1))
