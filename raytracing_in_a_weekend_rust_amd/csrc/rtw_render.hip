@@ -278,6 +278,8 @@ struct PathStack {
 // Diagnostic build only (-DRTW_STAMPS, librtw_stamps.so): per-wave s_memtime
 // cycle sums per section; never compiled into the product library.
 #ifdef RTW_STAMPS
+constexpr int kStampSlots = 10;  // diagnostic rows: [0, kStampSlots) sections, [14] count, [15] clock
+constexpr int kStampRow = 16;
 __device__ __forceinline__ uint64_t stamp_now() {
     uint64_t t;
     __builtin_amdgcn_sched_barrier(0);
@@ -286,7 +288,7 @@ __device__ __forceinline__ uint64_t stamp_now() {
     return t;
 }
 struct Stamps {
-    uint64_t last = stamp_now(), acc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t last = stamp_now(), acc[kStampSlots] = {};
 };
 #define STAMP(k)                                   \
     do {                                           \
@@ -357,7 +359,7 @@ struct PixelLoc {
 // camera.rs:400-420 + offset_lattice (422-450) + defocus_disk_sample (452-456):
 // the ray of lattice sample k; starts a fresh path.
 __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, uint32_t k, U128 &rng,
-                                        Path &p) {
+                                        Path &p, Stamps &stp) {
     double offx, offy, offz;
     if (P.s == 0) {
         offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
@@ -369,6 +371,7 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
         offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
     }
     const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
+    STAMP(8);  // 8: lattice sample position
     if (P.defocus_angle <= 0.) {
         p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
     } else {
@@ -386,6 +389,7 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
         p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
         p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
     }
+    STAMP(9);  // 9: defocus disk sample
     p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
     p.depth = 0;
     p.stk.clear();
@@ -397,7 +401,7 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
 __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restrict__ sph,
                                       const ShadeRec *__restrict__ shd, int best, double bt, double a,
                                       Path &p, U128 &rng, uint16_t *spill, uint64_t col, uint64_t stride,
-                                      double &lr, double &lg, double &lb) {
+                                      double &lr, double &lg, double &lb, Stamps &stp) {
     lr = lg = lb = 0.;
     if (best < 0) {
         const double uy = p.dy / __builtin_sqrt(a);
@@ -416,6 +420,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
     const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
     if (!front) nx = -nx, ny = -ny, nz = -nz;
+    STAMP(6);  // 6: hit record (point, normal, face)
     double ndx, ndy, ndz;
     if (M.kind != RTW_DIELECTRIC) {
         // Lambertian and Metal each draw exactly one random_unit_vec and nothing
@@ -503,7 +508,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
     const PixelLoc pl(P, x, y);
     const uint64_t stride = P.spill_stride;
     Path p;
-    gen_ray(P, pl, ps.k, ps.rng, p);
+    gen_ray(P, pl, ps.k, ps.rng, p, stp);
     STAMP(0);  // 0: seed jump + pixel setup
     for (;;) {
         // ---- Scene::hit (hittable.rs:131-143): first minimum over all spheres ----
@@ -513,13 +518,13 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
         STAMP(1);
         double lr, lg, lb;
-        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb);
+        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp);
         STAMP(3);  // 3: hit record + scatter / sky
         if (done) {
             fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
             if (++ps.k >= n_off) break;
             if (seg >= budget) return true;  // sample boundary: hand the rest to the coop kernel
-            gen_ray(P, pl, ps.k, ps.rng, p);
+            gen_ray(P, pl, ps.k, ps.rng, p, stp);
         }
         STAMP(4);  // 4: fold + next sample
     }
@@ -776,8 +781,8 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
 #ifdef RTW_STAMPS
     {  // max over lanes of each section sum -> one row per wave
         const uint32_t lane = threadIdx.x & 63u;
-        uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.y) * gridDim.x * 4 + blockIdx.x * 4 + threadIdx.x / 64u) * 8;
-        for (int k = 0; k < 6; ++k) {
+        uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.y) * gridDim.x * 4 + blockIdx.x * 4 + threadIdx.x / 64u) * kStampRow;
+        for (int k = 0; k < kStampSlots; ++k) {
             uint64_t v = stp.acc[k];
             for (int off = 32; off > 0; off >>= 1) {
                 const uint64_t o = __shfl_xor(v, off);
@@ -790,7 +795,7 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
             const uint64_t o = __shfl_xor(sm, off);
             sm = sm > o ? sm : o;
         }
-        if (lane == 0) row[6] = sm, row[7] = stamp_now();
+        if (lane == 0) row[14] = sm, row[15] = stamp_now();
     }
 #endif
     flush_tally(P, tl, true);
@@ -996,7 +1001,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
         uint32_t segs = 0;
         for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
             Path p;
-            gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p);
+            gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p, stp);
             for (;;) {  // one path (no spill: depth capped below the register slots)
                 ++segs;
                 const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
@@ -1005,7 +1010,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
                                          p.dz, a, bt, tl, stp);
                 if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
                 double cr, cg, cb;
-                shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb);
+                shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
             }
         }
         P.pcost[i] = segs;
@@ -1164,7 +1169,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         ps.k = P.n_off;
                         write_pixel(P, x, lr, ps);
                     } else {
-                        gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), 0, ps.rng, p);
+                        gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), 0, ps.rng, p, stp);
                         need = false;
                     }
                 } else {
@@ -1185,11 +1190,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
             STAMP(1);  // 1: hit tail (exact candidates, cut check)
             double cr, cg, cb;
-            const bool ended = shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb);
+            const bool ended = shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb, stp);
             STAMP(3);  // 3: hit record + scatter / sky
             if (ended) {
                 fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
                 acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
+                STAMP(7);  // 7: fold + pixel sum
                 const bool done = ++ps.k >= P.n_off;
                 // park: the budget is spent, the rate runs away, or -- once the
                 // cursor is dry, so drain groups are about to be plentiful -- the
@@ -1216,15 +1222,15 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     ++tl.parked;
                     need = true;
                 } else {
-                    gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, ps.rng, p);
+                    gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, ps.rng, p, stp);
                 }
             }
             STAMP(4);  // 4: fold + next sample / pixel end
         }
 #ifdef RTW_STAMPS
         {  // diagnostic: per cursor wave, the max over lanes of each section sum
-            uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.x) * (kThreads / 64u) + threadIdx.x / 64u) * 8;
-            for (int k = 0; k < 6; ++k) {
+            uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.x) * (kThreads / 64u) + threadIdx.x / 64u) * kStampRow;
+            for (int k = 0; k < kStampSlots; ++k) {
                 uint64_t v = stp.acc[k];
                 for (int off = 32; off > 0; off >>= 1) {
                     const uint64_t o = __shfl_xor(v, off);
@@ -1234,7 +1240,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             }
             uint32_t wi = tl.witer;  // wave iterations (counted on one lane each)
             for (int off = 32; off > 0; off >>= 1) wi += static_cast<uint32_t>(__shfl_xor(static_cast<int>(wi), off));
-            if (lane == 0) row[6] = wi, row[7] = stamp_now();
+            if (lane == 0) row[14] = wi, row[15] = stamp_now();
         }
 #endif
         // this wave parks no more (its parks are published: drained stores + flags)
@@ -1307,9 +1313,9 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
     }
 #ifdef RTW_STAMPS
     if ((threadIdx.x & 63u) == 0) {  // diagnostic: per-wave rows after the tile kernel's
-        uint64_t *row = P.stamps_coop + (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64u) + threadIdx.x / 64u) * 8;
-        for (int k = 0; k < 6; ++k) row[k] = stp.acc[k];
-        row[6] = seg, row[7] = stamp_now();
+        uint64_t *row = P.stamps_coop + (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64u) + threadIdx.x / 64u) * kStampRow;
+        for (int k = 0; k < kStampSlots; ++k) row[k] = stp.acc[k];
+        row[14] = seg, row[15] = stamp_now();
     }
 #endif
     tl.seg = seg;
@@ -1613,14 +1619,14 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         const size_t nw = nt + static_cast<size_t>(kCoopBlocks) * (kBlock / 64);  // + phase-2 waves
         static uint64_t *d_st = nullptr;
         static size_t cap = 0;
-        if (nw * 64 > cap) {
+        if (nw * kStampRow * 8 > cap) {
             if (d_st) (void)hipFree(d_st);
-            HIPCHECK(hipMalloc(&d_st, nw * 64));
-            cap = nw * 64;
+            HIPCHECK(hipMalloc(&d_st, nw * kStampRow * 8));
+            cap = nw * kStampRow * 8;
         }
-        HIPCHECK(hipMemset(d_st, 0, nw * 64));
+        HIPCHECK(hipMemset(d_st, 0, nw * kStampRow * 8));
         P.stamps = d_st;
-        P.stamps_coop = d_st + nt * 8;
+        P.stamps_coop = d_st + nt * kStampRow;
         stamp_buf() = d_st;
         stamp_n() = nw;
     }
@@ -1992,7 +1998,7 @@ int rtw_diag_stamps(uint64_t *out, uint64_t cap_rows, uint64_t *n_rows) {
     *n_rows = stamp_n();
     if (!out || cap_rows < stamp_n()) return RTW_E_CAPACITY;
     (void)hipDeviceSynchronize();
-    return hipMemcpy(out, stamp_buf(), stamp_n() * 64, hipMemcpyDeviceToHost) == hipSuccess ? RTW_OK : RTW_E_HIP;
+    return hipMemcpy(out, stamp_buf(), stamp_n() * kStampRow * 8, hipMemcpyDeviceToHost) == hipSuccess ? RTW_OK : RTW_E_HIP;
 }
 #endif
 

@@ -19,15 +19,15 @@ f = capi.lib.rtw_diag_stamps
 f.argtypes = [C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64)]
 nr = C.c_uint64()
 f(None, 0, C.byref(nr))
-buf = np.zeros((nr.value, 8), dtype=np.uint64)
+buf = np.zeros((nr.value, 16), dtype=np.uint64)
 assert f(buf.ctypes.data_as(C.POINTER(C.c_uint64)), nr.value, C.byref(nr)) == 0
 names = ["setup", "hit-tail", "walk", "scatter", "fold+next", "seg+always"]
 nt = ((W + 15) // 16) * 1 * 4  # tile-kernel rows (one image row), then phase-2 waves
 print(f"kernel {st.kernel_ms:.2f} ms, segments {st.segments}, accel {st.accel}, parked {st.parked_pixels}")
 for label, rows in (("tile", buf[:nt]), ("coop", buf[nt:])):
-    life = rows[:, :6].sum(axis=1).astype(np.float64)
+    life = rows[:, :10].sum(axis=1).astype(np.float64)
     for w in np.argsort(-life)[:3]:
-        segs = float(rows[w, 6])
+        segs = float(rows[w, 14])
         print(f"{label} wave {int(w)}: life {life[w] / 1e6:.2f} Mcyc, max-lane segments {segs:.0f}, "
               f"{life[w] / max(1., segs):.0f} cyc/segment:",
               ", ".join(f"{nme} {float(rows[w, k]) / max(1., segs):.0f}" for k, nme in enumerate(names)))

@@ -17,11 +17,11 @@ f = capi.lib.rtw_diag_stamps
 f.argtypes = [C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64)]
 nr = C.c_uint64()
 f(None, 0, C.byref(nr))
-buf = np.zeros((nr.value, 8), dtype=np.uint64)
+buf = np.zeros((nr.value, 16), dtype=np.uint64)
 rc = f(buf.ctypes.data_as(C.POINTER(C.c_uint64)), nr.value, C.byref(nr))
 assert rc == 0, rc
 names = ["setup", "hit-tail", "walk", "hit+scatter", "fold+next", "seg+always"]
-tot = buf[:, :6].sum(axis=0).astype(np.float64)
+tot = buf[:, :10].sum(axis=0).astype(np.float64)
 print(f"s={s} kernel_ms={st.kernel_ms:.1f} waves={nr.value} segments={st.segments} wave_iters={st.wave_iterations}")
 print(f"walk: lane visits/segment {st.node_visits / max(1, st.segments):.2f} (wrapped 16-bit per lane: lower bound); "
       f"wave-level walk iterations/wave-iter {st.brute_segments / max(1, st.wave_iterations):.2f}")
@@ -30,8 +30,8 @@ for k, nme in enumerate(names):
 print(f"  total per wave-iter {tot.sum()/st.wave_iterations:.0f} cycles; waves resident-equivalent "
       f"{tot.sum() / (st.kernel_ms * 1e-3 * 2.4e9 * 1024):.2f} per SIMD (at 2.4 GHz)")
 
-life = buf[:, :6].sum(axis=1).astype(np.float64)
-segmax = buf[:, 6].astype(np.float64)
+life = buf[:, :10].sum(axis=1).astype(np.float64)
+segmax = buf[:, 14].astype(np.float64)
 order = np.argsort(-life)
 print("per-wave lifetime (Mcycles): mean %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f; kernel %.1f Mcycles@2.4GHz"
       % (life.mean() / 1e6, np.percentile(life, 50) / 1e6, np.percentile(life, 90) / 1e6,

@@ -17,13 +17,14 @@ f = capi.lib.rtw_diag_stamps
 f.argtypes = [C.POINTER(C.c_uint64), C.c_uint64, C.POINTER(C.c_uint64)]
 nr = C.c_uint64()
 f(None, 0, C.byref(nr))
-buf = np.zeros((nr.value, 8), dtype=np.uint64)
+buf = np.zeros((nr.value, 16), dtype=np.uint64)
 assert f(buf.ctypes.data_as(C.POINTER(C.c_uint64)), nr.value, C.byref(nr)) == 0
 rows = buf[: st.grid_blocks * 12]
-rows = rows[rows[:, 6] > 0]
-names = ["loop top/refill", "hit tail", "walk", "scatter", "fold+next", "seg setup+always"]
-tot = rows[:, :6].sum(axis=0).astype(np.float64)
-wi = float(rows[:, 6].sum())
+rows = rows[rows[:, 14] > 0]
+names = ["loop top/refill", "hit tail", "walk", "scatter (after record)", "next sample/pixel", "seg setup+always",
+         "hit record", "fold+sum", "lattice position", "defocus disk"]
+tot = rows[:, :10].sum(axis=0).astype(np.float64)
+wi = float(rows[:, 14].sum())
 print(f"s={s} kernel_ms={st.kernel_ms:.1f} cursor waves={len(rows)} wave iterations={wi:.0f} "
       f"segments={st.segments} (per wave-iter {st.segments / wi:.1f} lanes)")
 for k, nme in enumerate(names):
