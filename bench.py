@@ -41,6 +41,9 @@ FLOP_PER_VISIT = 20  # BVH walk step: slab test 6 FMA + 10 min/max, or the 17-FL
 FP32_VECTOR_PEAK = 157.3  # TFLOP/s, MI355X spec (MI355X_MICROARCH.md chip table)
 FP64_VECTOR_PEAK = 78.6   # TFLOP/s, MI355X spec
 PMC_FILE = os.path.join(HERE, "profiles", "pmc_traffic.json")
+INSTS_FILE = os.path.join(HERE, "profiles", "pmc_insts.json")
+GPU_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
+VALU_CYCLES = 4       # a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles
 
 
 def parse():
@@ -147,6 +150,21 @@ def main():
     else:
         flop = brute_flop
     achieved = flop / (kms / 1e3) / 1e12
+    valu = None  # VALU issue utilisation from the committed PMC pass (profiles/pmc_insts.json)
+    if os.path.exists(INSTS_FILE) and world == 1:
+        try:
+            with open(INSTS_FILE) as f:
+                pi = json.load(f)
+            if pi.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}":
+                n_valu = pi["sq_insts_valu_per_launch"]
+                simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+                peak = simds * GPU_CLOCK_HZ / VALU_CYCLES / 1e9  # wave-instructions per second (G)
+                ach = n_valu / (kms / 1e3) / 1e9
+                valu = {"insts_per_launch": n_valu, "achieved": round(ach, 2), "peak": round(peak, 2),
+                        "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
+                        "per_wave_segment": round(n_valu / max(1, st.segments / 64), 1)}
+        except Exception:
+            valu = None
     traffic = None
     if os.path.exists(PMC_FILE):
         try:
@@ -189,7 +207,10 @@ def main():
                                   "kernel time") +
                                  "; the per-ray tests run in f32 (exact-conservative), so peak = FP32 "
                                  "vector; brute_force_equiv_tflops = SURVEY 8(d)'s segments x N x 17 "
-                                 "over the same time; the kernel is latency-bound (DESIGN.md 4)"},
+                                 "over the same time. What bounds the launch is VALU issue: "
+                                 "valu_issue = committed PMC SQ_INSTS_VALU per launch x 4 cycles over "
+                                 "SIMDs x clock x kernel time (DESIGN.md 4)",
+                         "valu_issue": valu},
             "stats": {"accel": ["scan_f64", "scan_f32_filter", "bvh"][st.accel],
                       "node_visits_per_segment": round(st.node_visits / max(1, st.segments), 3),
                       "brute_segments": st.brute_segments, "lds_bytes": st.lds_bytes,

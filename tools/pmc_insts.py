@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Per-launch instruction counts of the persistent render kernel from a rocprofv3
+--pmc pass (SQ_INSTS_* count wave-level instructions). The bulk of the launch is
+VALU-issue bound: one wave64 VALU instruction occupies a SIMD for 4 cycles, so
+issue utilisation = VALU x 4 / (SIMDs x clock x kernel time).
+Usage: pmc_insts.py OUTDIR  (expects OUTDIR/pmc_insts)."""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNEL = "rtw_render_persist"
+
+
+def main():
+    out = sys.argv[1]
+    acc, launches = {}, {}
+    for f in glob.glob(os.path.join(out, "pmc_insts", "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if KERNEL in row["Kernel_Name"]:
+                    n = row["Counter_Name"]
+                    acc[n] = acc.get(n, 0.0) + float(row["Counter_Value"])
+                    launches.setdefault(n, set()).add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+    res = {"workload": "complex_1200x675_s23_d50", "kernel": KERNEL}
+    for n, v in sorted(acc.items()):
+        res[n.lower() + "_per_launch"] = v / max(1, len(launches[n]))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
