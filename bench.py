@@ -6,11 +6,17 @@ scene (raytracing::complex, raytracing/mod.rs:54-126; 486 spheres at the fixed
 scene seed), 1200x675, spp=500 -> samples_sqrt 23 (529 spp, the reference API
 takes samples_sqrt), max_depth 50, f64 parity mode (bit-identical to the
 reference restatement). One step = one whole-image render (Camera::threaded_render
-equivalent) with the scene already resident in HBM; for N>1 the image is
-row-cyclically sharded over the ranks and gathered to rank 0 over RCCL
-(all_gather of the row tiles) inside the timed step.
+equivalent) with the scene already resident in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+N>1 (one rank per GPU): by default weak scaling -- the job renders N frames, rank r
+frame r (render seed SEED + r, shard.frame_seed), each a full 1200x675 spp-529
+image, with no data-path collective (frames are independent).
+`--scaling strong` renders the ONE frame row-cyclically sharded over the ranks and
+gathered over RCCL (all_gather of the row tiles) inside the timed step: BASELINE
+configs[3]'s scaling curve, whose per-rank times the serial per-pixel RNG chains
+bound.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints one JSON line (contract in the task statement). The cpu_baseline
@@ -43,7 +49,12 @@ FP64_VECTOR_PEAK = 78.6   # TFLOP/s, MI355X spec
 PMC_FILE = os.path.join(HERE, "profiles", "pmc_traffic.json")
 INSTS_FILE = os.path.join(HERE, "profiles", "pmc_insts.json")
 GPU_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
-VALU_CYCLES = 4       # a wave64 VALU instruction occupies a 16-lane SIMD for 4 cycles
+# gfx950 VALU issue (MI355X_MICROARCH.md cycle constants): a wave64 f32/int VALU
+# instruction occupies the 32-lane SIMD for 2 cycles; f64 FMA/MUL/ADD run at half
+# rate (4 cycles: FP64 vector peak = 1/2 FP32); one wave alone issues at most one
+# VALU instruction per 4 cycles.
+VALU_CYCLES = 2
+VALU_CYCLES_F64 = 4
 
 
 def parse():
@@ -52,6 +63,9 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--samples-sqrt", type=int, default=SQRT)
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="N>1: weak = one whole frame per rank (seed SEED+rank), no collective; "
+                        "strong = the one frame row-cyclically sharded + RCCL all_gather")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU leg")
     p.add_argument("--cpu-row-stride", type=int, default=0,
                    help="oracle renders every k-th row (0 = auto, ~10-30 s)")
@@ -95,13 +109,19 @@ def main():
     s = a.samples_sqrt
     cam, sph, ns, mt, nm = rtw.builtin_scene("complex", SEED, H, W, DEPTH)
     n_off = s * s if s else 1
-    rb, rstep, rows_local = shard.rows_of(rank, world, H)
-    rm = shard.rows_max(world, H)
+    weak = a.scaling == "weak"
+    if weak:  # frame `rank` of an N-frame job, the whole image on this rank
+        rb, rstep, rows_local, rm = 0, 1, H, H
+        render_seed = shard.frame_seed(SEED, rank)
+    else:  # row-cyclic shard of the one frame
+        rb, rstep, rows_local = shard.rows_of(rank, world, H)
+        rm = shard.rows_max(world, H)
+        render_seed = SEED
     sess = rtw.Session(local)
     sess.set_scene(sph, ns, mt, nm)
     dev = torch.device("cuda", local)
     fb = torch.zeros((rm, W, 3), dtype=torch.float64, device=dev)  # padded tile
-    if world > 1:
+    if world > 1 and not weak:
         gathered = torch.empty((world * rm, W, 3), dtype=torch.float64, device=dev)
         image = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
         index = shard.unpermute_index(world, H, dev)
@@ -112,10 +132,10 @@ def main():
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
-        sess.render(cam.raw, s, SEED, fb.data_ptr(), stream=stream.cuda_stream,
+        sess.render(cam.raw, s, render_seed, fb.data_ptr(), stream=stream.cuda_stream,
                     shard=(rb, rstep, rows_local))
         ev1.record(stream)
-        if world > 1:  # RCCL all_gather of the row tiles + un-permute
+        if world > 1 and not weak:  # RCCL all_gather of the row tiles + un-permute
             shard.gather_image(fb, world, H, gathered, image, index)
         if record:
             kernel_ms.append((ev0, ev1))
@@ -139,7 +159,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    total_samples = W * H * n_off * a.steps
+    frames = world if weak else 1
+    total_samples = frames * W * H * n_off * a.steps
     value = total_samples / elapsed / 1e6
     brute_flop = st.sphere_tests * FLOP_PER_TEST  # segments x N x 17, per launch
     if st.accel == 2:
@@ -157,12 +178,21 @@ def main():
                 pi = json.load(f)
             if pi.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}":
                 n_valu = pi["sq_insts_valu_per_launch"]
+                n_f64 = sum(pi.get(k, 0.) for k in ("sq_insts_valu_fma_f64_per_launch",
+                                                    "sq_insts_valu_mul_f64_per_launch",
+                                                    "sq_insts_valu_add_f64_per_launch",
+                                                    "sq_insts_valu_trans_f64_per_launch"))
                 simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
-                peak = simds * GPU_CLOCK_HZ / VALU_CYCLES / 1e9  # wave-instructions per second (G)
-                ach = n_valu / (kms / 1e3) / 1e9
-                valu = {"insts_per_launch": n_valu, "achieved": round(ach, 2), "peak": round(peak, 2),
-                        "unit": "G wave-instr/s", "frac": round(ach / peak, 3),
-                        "per_wave_segment": round(n_valu / max(1, st.segments / 64), 1)}
+                # SIMD cycles the launch's VALU instructions occupy, over the SIMD-cycles available
+                busy = VALU_CYCLES * (n_valu - n_f64) + VALU_CYCLES_F64 * n_f64
+                avail = simds * GPU_CLOCK_HZ * (kms / 1e3)
+                valu = {"insts_per_launch": n_valu, "f64_insts_per_launch": n_f64,
+                        "achieved": round(n_valu / (kms / 1e3) / 1e9, 2),
+                        "unit": "G wave-instr/s", "simd_busy_frac": round(busy / avail, 3),
+                        "per_wave_segment": round(n_valu / max(1, st.segments / 64), 1),
+                        "note": "simd_busy_frac = (2 cyc x f32/int + 4 cyc x f64 VALU instructions, PMC "
+                                "SQ_INSTS_VALU*) / (SIMDs x clock x kernel time); profiles/pmc_insts.json "
+                                "is from the profiled build"}
         except Exception:
             valu = None
     traffic = None
@@ -186,18 +216,20 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (the reference's own procedural final scene, fixed seed)",
             "config": {"workload": f"complex_{W}x{H}_s{s}_d{DEPTH}", "width": W, "height": H,
                        "samples_sqrt": s, "spp": n_off, "max_depth": DEPTH,
-                       "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED,
-                       "parallelism": f"row-cyclic x{world}" + (" + rccl all_gather" if world > 1 else ""),
+                       "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED, "frames": frames,
+                       "parallelism": (f"frame-per-rank x{world} (render seed SEED+rank), no collective"
+                                       if weak else f"row-cyclic x{world}" +
+                                       (" + rccl all_gather" if world > 1 else "")),
                        "mode": "parity_f64 (bit-exact)"},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP32_VECTOR_PEAK,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_VECTOR_PEAK, 4),
-                         "traffic": traffic, "kernel": "rtw_render_f64",
+                         "traffic": traffic, "kernel": "rtw_render_persist (+ 7 small launches)",
                          "kernel_ms": round(kms, 3),
                          "flop_per_launch": flop,
                          "brute_force_equiv_tflops": round(brute_flop / (kms / 1e3) / 1e12, 3),
@@ -207,9 +239,8 @@ def main():
                                   "kernel time") +
                                  "; the per-ray tests run in f32 (exact-conservative), so peak = FP32 "
                                  "vector; brute_force_equiv_tflops = SURVEY 8(d)'s segments x N x 17 "
-                                 "over the same time. What bounds the launch is VALU issue: "
-                                 "valu_issue = committed PMC SQ_INSTS_VALU per launch x 4 cycles over "
-                                 "SIMDs x clock x kernel time (DESIGN.md 4)",
+                                 "over the same time. Neither is the bound: divergent per-lane work "
+                                 "at 3 waves/SIMD is VALU-issue + latency bound (valu_issue, DESIGN.md 4)",
                          "valu_issue": valu},
             "stats": {"accel": ["scan_f64", "scan_f32_filter", "bvh"][st.accel],
                       "node_visits_per_segment": round(st.node_visits / max(1, st.segments), 3),
@@ -218,7 +249,9 @@ def main():
                       "segments": st.segments, "segments_per_sample": round(st.segments / max(1, st.samples), 4),
                       "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
-                      "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3)},
+                      "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
+                      "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),
+                      "trap_skipped_fraction": round(st.trap_segments / max(1, st.segments), 4)},
         }
     if rank == 0 and world == 1 and a.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)

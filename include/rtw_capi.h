@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
+#define RTW_ABI_VERSION 3
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -95,6 +95,8 @@ typedef struct rtw_stats {
     uint32_t accel;           /* 0 brute-force f64, 1 f32-filtered scan, 2 BVH         */
     uint32_t lds_bytes;       /* dynamic LDS per workgroup                             */
     uint64_t parked_pixels;   /* pixels finished by the cooperative second kernel      */
+    uint64_t inside_segments; /* segments resolved by the inside cut (rtw_accel.h)     */
+    uint64_t trap_segments;   /* segments skipped by the trapped-path fast-forward      */
 } rtw_stats;
 
 /* ---- library ---- */

@@ -71,7 +71,8 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("grid_blocks", C.c_uint32),
                 ("block_threads", C.c_uint32), ("node_visits", C.c_uint64),
                 ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32),
-                ("parked_pixels", C.c_uint64)]
+                ("parked_pixels", C.c_uint64), ("inside_segments", C.c_uint64),
+                ("trap_segments", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -227,4 +227,74 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     return true;
 }
 
+// Inside-cut lists (rtw_accel.h): for every sphere S the spheres T whose gap to S
+// is within delta(S, T); lists longer than kMaxNbr (e.g. a ground sphere with
+// every small sphere resting on it) get no cut. O(n^2) pairs, scenes of up to
+// 8192 spheres; larger ones (and any non-finite sphere) get no cuts.
+void build_inside(const double *centers, const double *radii, uint32_t n, std::vector<uint32_t> &info,
+                  std::vector<uint16_t> &ids, const uint8_t *trap_ok, std::vector<TrapRec> *trap) {
+    info.assign(n, kNbrNone);
+    ids.clear();
+    if (trap) trap->assign(n, TrapRec{0., 0., 0., kTrapNever});
+    if (n > 8192) return;
+    std::vector<double> m(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const double *ci = centers + 3 * i;
+        m[i] = std::max(std::max(std::fabs(ci[0]), std::fabs(ci[1])), std::fabs(ci[2]));
+        if (!std::isfinite(m[i]) || !std::isfinite(radii[i]) || m[i] > 1e12 || std::fabs(radii[i]) > 1e12) return;
+    }
+    std::vector<uint32_t> nb;
+    std::vector<double> nb_delta;
+    for (uint32_t s = 0; s < n; ++s) {
+        nb.clear(), nb_delta.clear();
+        const double rs = std::fabs(radii[s]);
+        for (uint32_t t = 0; t < n; ++t) {
+            if (t == s) continue;
+            const double rt = std::fabs(radii[t]);
+            double d2 = 0.;
+            for (int k = 0; k < 3; ++k) {
+                const double q = centers[3 * s + k] - centers[3 * t + k];
+                d2 += q * q;
+            }
+            const double D = std::sqrt(d2);
+            const double delta = kNbrMargin * (5. * rs + 2. * rt + D + m[s] + m[t]);
+            if (D - rs - rt <= delta) nb.push_back(t), nb_delta.push_back(delta);
+        }
+        if (nb.size() <= kMaxNbr) {
+            info[s] = (static_cast<uint32_t>(ids.size()) << 8) | static_cast<uint32_t>(nb.size());
+            for (uint32_t t : nb) ids.push_back(static_cast<uint16_t>(t));
+        }
+        if (!trap || !trap_ok || !trap_ok[s] || !(radii[s] >= 0.02)) continue;
+        TrapRec &tr = (*trap)[s];
+        if (nb.empty()) {
+            tr = TrapRec{0., 0., 0., 1.};
+            continue;
+        }
+        // w: mean direction towards the neighbours; every neighbour point x has
+        // (x - c_S).w >= (c_T - c_S).w - r_T, so chords with both ends below
+        // m = the minimum of that less delta stay delta clear of all of them
+        double w[3] = {0., 0., 0.};
+        bool ok = true;
+        for (uint32_t t : nb) {
+            double q[3], D = 0.;
+            for (int k = 0; k < 3; ++k) q[k] = centers[3 * t + k] - centers[3 * s + k], D += q[k] * q[k];
+            D = std::sqrt(D);
+            if (!(D > 1e-9 * (rs + 1.))) ok = false;
+            for (int k = 0; k < 3; ++k) w[k] += q[k] / D;
+        }
+        const double wl = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        if (!ok || !(wl > 1e-6)) continue;
+        for (double &x : w) x /= wl;
+        double mm = INFINITY;
+        for (size_t j = 0; j < nb.size(); ++j) {
+            const uint32_t t = nb[j];
+            double proj = 0.;
+            for (int k = 0; k < 3; ++k) proj += (centers[3 * t + k] - centers[3 * s + k]) * w[k];
+            mm = std::min(mm, proj - std::fabs(radii[t]) - nb_delta[j]);
+        }
+        const double cap = mm / rs - 1e-9;
+        if (cap > -0.999) tr = TrapRec{w[0], w[1], w[2], std::min(cap, 1.)};
+    }
+}
+
 }  // namespace rtw_accel

@@ -347,6 +347,79 @@ RTW_HD bool better(double t, uint32_t i, double bt, int best) {
     return best < 0 || t < bt || (t == bt && static_cast<int>(i) < best);
 }
 
+// ---- Inside cut: a segment that starts inside the sphere it last hit ----------
+// Rays trapped inside a sphere (refracted into glass, or scattered inward from
+// the inner face of any sphere -- the reference flips the normal, hittable.rs:
+// 64-81, so a Lambertian bounce from inside stays inside) make up most of the
+// heaviest pixels' segments. If sphere S's near root is rejected (t < 0.01,
+// interval.rs:55-57) and its far root t_f accepted, every ray point with
+// t in [0.01, t_f] lies within S (up to the roots' rounding error), so a sphere
+// T can beat t_f only if it comes within that error of S. The host lists, per S,
+// the spheres with gap |c_S - c_T| - |r_S| - |r_T| <= delta(S, T) (overlapping or
+// nearly touching); the segment's exact result is then the (t, index) minimum
+// over S and its list -- the scan's first minimum, since every other sphere's
+// accepted root is strictly beyond t_f.
+//
+// delta: the f64 root of Sphere::hit errs in distance by at most about
+// sqrt(12u)(|oc| + r) = 2^-24.5 (|oc| + r) (tangent rays: the discriminant's
+// error 12u|d|^2(|oc|^2 + r^2) under the square root; u = 2^-53). The device takes
+// the cut only when |o - c_S|^2 - r_S^2 <= 3 r_S^2, so |oc_S| <= 2|r_S| and
+// |oc_T| <= 2|r_S| + D; delta = 2^-20 (5|r_S| + 2|r_T| + D + |c_S| + |c_T|) is
+// over 20x the sum of both roots' errors.
+constexpr uint32_t kNbrNone = 0xffffffffu;  // ShadeRec info word: no inside cut for this sphere
+constexpr uint32_t kMaxNbr = 8;             // longer lists take the normal walk
+constexpr double kNbrMargin = 9.5367431640625e-07;  // 2^-20
+
+// Sphere::hit of sphere (c, rr) when the ray starts inside it: true iff the
+// discriminant is non-negative, |oc|^2 - rr <= 3 rr, the near root is rejected
+// and the far root accepted; t = the far root, computed exactly as
+// sphere_hit_f64 computes it (same operations, same order).
+RTW_HD bool inside_far(double ox, double oy, double oz, double dx, double dy, double dz, double a,
+                       double cx, double cy, double cz, double rr, double &t) {
+    const double ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const double hb = ocx * dx + ocy * dy + ocz * dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rr;
+    // cheap exits first: origin far out, or on/outside S heading away (hb >= 0
+    // with c >= 0 puts both roots at or below ~0: the cut never applies)
+    if (!(c <= 3. * rr) || (hb >= 0. && c >= 0.)) return false;
+    const double disc = hb * hb - a * c;
+    if (!(disc >= 0.)) return false;
+    const double sq = __builtin_sqrt(disc);
+    if ((-sq - hb) / a >= 0.01) return false;  // entering from outside: the normal path
+    t = (sq - hb) / a;
+    return t >= 0.01;
+}
+
+// ---- Trapped paths -------------------------------------------------------------
+// Lambertian: a bounce off the inner face of sphere S (front_face false, so the
+// reference flips the normal inward, hittable.rs:64-81) scatters along
+// d = n_in + u (materials.rs:22-37, u = random_unit_vec). From a surface point
+// o = c + r h0 the far root along d is exactly t = r, and the ray ends at c + r u:
+// a uniformly random point of S. Unless a neighbour comes nearer, the path stays
+// inside S bounce after bounce until the depth cap returns black (camera.rs:
+// 381-383); only its RNG draws (random_unit_vec's rejection loop, vec3.rs:218-232,
+// which does not depend on the geometry) and its segment count matter.
+// Dielectric: total internal reflection inside a sphere keeps its angle (the
+// chords of a sphere are isosceles), draws nothing (the reflectance draw is
+// short-circuited, materials.rs:96-98) and walks a great circle of S.
+// The host gives every sphere S that can trap (r >= 0.02, so chords of t = r,
+// 2r or 2r cos stay far above 0.01; Lambertian albedo finite and >= +0 so the
+// dropped factors of the black product change no bit) a half-space
+// {(x - c).w < r cap} that keeps every chord inside S at least delta away from
+// each neighbour (w = 0, cap = 1: no neighbours; cap <= -2: never). The device
+// checks each chord end against it and falls back to tracing on any doubt.
+struct TrapRec {
+    double wx, wy, wz, cap;
+};
+constexpr double kTrapNever = -3.;
+
+// Host: per sphere the info word (offset << 8 | count into `ids`, or kNbrNone)
+// of its inside-cut list; with `trap_ok` (per sphere: may trap) also its TrapRec.
+// Scenes with a non-finite sphere get no cuts and no traps.
+void build_inside(const double *centers, const double *radii, uint32_t n, std::vector<uint32_t> &info,
+                  std::vector<uint16_t> &ids, const uint8_t *trap_ok = nullptr,
+                  std::vector<TrapRec> *trap = nullptr);
+
 // ---- host only (declared in both compilation passes, defined for the host) ----
 // R2' of the pass-1 record of a sphere (center c, r*r = rr); +inf (always tested
 // exactly) outside the guard or for non-finite input.

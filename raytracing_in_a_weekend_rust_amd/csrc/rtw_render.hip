@@ -49,7 +49,7 @@ constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
-constexpr int kCounters = 8;
+constexpr int kCounters = 10;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
 constexpr uint32_t kTailSegs = 768;     // dry-cursor parking: estimated segments left (RTW_TAIL)
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
@@ -94,10 +94,12 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
 // Per-sphere shading record (48 B): the sphere's radius and its material row
-// flattened (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric).
+// flattened (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric);
+// nbr = the sphere's inside-cut list (offset << 8 | count into KParams::nbr, or
+// rtw_accel::kNbrNone; rtw_accel.h "Inside cut").
 struct ShadeRec {
     double r, a0, a1, a2, p;
-    uint32_t kind, _pad;
+    uint32_t kind, nbr;
 };
 
 struct KParams {
@@ -112,6 +114,8 @@ struct KParams {
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
     uint32_t tail_segs, _pad5;  // once the cursor is dry: park pixels with more estimated work left
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
+    uint32_t n_nbr;             // inside-cut list entries
+    uint32_t inside_cursor;     // 1: one-lane-per-pixel paths try the inside cut (drain groups always do)
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -119,6 +123,8 @@ struct KParams {
     const float4 *leaves;       // BVH leaves, 2 float4 each
     const uint32_t *always;     // spheres tested exactly before the walk
     const ShadeRec *shade;      // per-sphere radius + material
+    const uint16_t *nbr;        // inside-cut lists (ShadeRec::nbr indexes them)
+    const double4 *trap;        // per sphere rtw_accel::TrapRec {w, cap}
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
     uint16_t *spill;            // path-stack levels >= kRegSlots, region A: [level][pixel]
@@ -142,7 +148,8 @@ struct KParams {
     uint32_t *pixels_done;      // pixels written (completeness check of the persistent kernel)
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
                                    // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
-                                   // [6] parked pixels, [7] queue spin timeouts
+                                   // [6] parked pixels, [7] queue spin timeouts, [8] inside cuts,
+                                   // [9] segments skipped by the trapped-path fast-forward
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -320,16 +327,23 @@ struct Parked {
 };
 
 // Scene data a kernel reads per segment: f64 sphere records, shading records,
-// BVH nodes + leaves -- in LDS when they fit (kLds), else in HBM.
+// BVH nodes + leaves, inside-cut lists -- in LDS when they fit (kLds), else in HBM.
 struct SceneView {
     const double4 *sph;
     const ShadeRec *shd;
     const float4 *nodes, *leaves;
+    const uint16_t *nbr;
 };
-// LDS layout: [n] double4 sph | [n] ShadeRec | (BVH) [8 n_node] + [2 n_leaf] float4
-__host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh) {
+// inside-cut list entries (u16) in float4 units
+__host__ __device__ constexpr uint32_t nbr_f4(uint32_t n_nbr) { return (n_nbr + 7u) / 8u; }
+// LDS layout: [n] double4 sph | [n] ShadeRec | (BVH) [9 n_node] + [2 n_leaf] float4 +
+// inside-cut lists (padded to float4)
+__host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh,
+                                                uint32_t n_nbr = 0) {
     return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
-           (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf)) * sizeof(float4) : 0);
+           (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf) +
+                   nbr_f4(n_nbr)) * sizeof(float4)
+                : 0);
 }
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
 // sum (3 x f64 columns) and the BVH walk scratch (kScratch x u16 columns).
@@ -341,6 +355,7 @@ __host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
 struct Path {
     double ox, oy, oz, dx, dy, dz;
     uint32_t depth;
+    int prev;  // sphere of the last hit (-1: camera ray): the inside-cut hint
     PathStack stk;
 };
 
@@ -392,20 +407,40 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
     STAMP(9);  // 9: defocus disk sample
     p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
     p.depth = 0;
+    p.prev = -1;
     p.stk.clear();
 }
+
+// What a scatter tells the trapped-path fast-forward (rtw_accel.h "Trapped
+// paths"): a Lambertian bounce off S's inner face (lam) or a total internal
+// reflection inside S (tir), S's outward normal h0 at the hit, and for Lambertian
+// the unit vector u, whether near_zero replaced the direction, and |d|^2.
+struct TrapHint {
+    bool lam = false, tir = false, quirk = false;
+    double h0x = 0., h0y = 0., h0z = 0., ux = 0., uy = 0., uz = 0., a1 = 0.;
+};
 
 // After Scene::hit: HitRecord + Material::scatter (materials.rs:22-111) on a hit,
 // the sky colour (camera.rs:395-397) on a miss. Returns true when the sample's
 // path ended (sky, or depth cap -> black); then (lr, lg, lb) is the leaf colour.
+// unit(dir) (vec3.rs:183-185) is formed once for whichever of the sky, Metal
+// (materials.rs:55) and Dielectric (materials.rs:91) the wave's lanes need, and
+// the reflection (vec3.rs:252-257) once for Metal and reflecting Dielectric lanes.
+// With kTrap the scatter also fills *th (trapped-path hints).
+template <bool kTrap = false>
 __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restrict__ sph,
                                       const ShadeRec *__restrict__ shd, int best, double bt, double a,
                                       Path &p, U128 &rng, uint16_t *spill, uint64_t col, uint64_t stride,
-                                      double &lr, double &lg, double &lb, Stamps &stp) {
+                                      double &lr, double &lg, double &lb, Stamps &stp, TrapHint *th = nullptr) {
     lr = lg = lb = 0.;
+    const uint32_t kind = best >= 0 ? shd[best].kind : 3u;  // 3: the sky
+    double vx = 0., vy = 0., vz = 0.;
+    if (kind != RTW_LAMBERTIAN) {
+        const double l = __builtin_sqrt(a);
+        vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+    }
     if (best < 0) {
-        const double uy = p.dy / __builtin_sqrt(a);
-        const double t = 0.5 * (uy + 1.0);
+        const double t = 0.5 * (vy + 1.0);
         const double om = 1.0 - t;
         lr = om + 0.5 * t;
         lg = om + 0.7 * t;
@@ -419,55 +454,107 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     const double px = p.dx * bt + p.ox, py = p.dy * bt + p.oy, pz = p.dz * bt + p.oz;
     double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
     const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
+    if constexpr (kTrap) th->h0x = nx, th->h0y = ny, th->h0z = nz;
     if (!front) nx = -nx, ny = -ny, nz = -nz;
     STAMP(6);  // 6: hit record (point, normal, face)
-    double ndx, ndy, ndz;
-    if (M.kind != RTW_DIELECTRIC) {
+    double ux = 0., uy = 0., uz = 0.;
+    if (kind != RTW_DIELECTRIC) {
         // Lambertian and Metal each draw exactly one random_unit_vec and nothing
         // else from the RNG: one rejection loop serves both (less divergence)
-        double ux, uy, uz;
         random_unit_vec(rng, ux, uy, uz);
-        if (M.kind == RTW_LAMBERTIAN) {  // materials.rs:22-37
-            ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
-            if (ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = nx, ndy = ny, ndz = nz;
-        } else {  // Metal, materials.rs:52-63
-            const double l = __builtin_sqrt(a);
-            const double vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
-            const double dt = vx * nx + vy * ny + vz * nz;
-            const double rx = vx - (nx * dt) * 2., ry = vy - (ny * dt) * 2., rz = vz - (nz * dt) * 2.;
-            ndx = rx + ux * M.p, ndy = ry + uy * M.p, ndz = rz + uz * M.p;
-        }
-        p.stk.push(static_cast<uint32_t>(best), spill, stride, col);  // attenuation row
-    } else {  // Dielectric, materials.rs:83-111 (attenuation 1: exact no-op)
-        const double ir = M.p;
-        const double ratio = front ? 1. / ir : ir;
-        const double l = __builtin_sqrt(a);
-        const double vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
-        const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+    }
+    bool refl = kind == RTW_METAL;
+    double ratio = 0., cos_t = 0.;
+    if (kind == RTW_DIELECTRIC) {  // materials.rs:83-111 (attenuation 1: exact no-op)
+        // M.a0 = 1/ir and M.a1 = r0*r0 of reflectance (75-80), formed by the host
+        // with the reference's own IEEE operations: the same bits
+        ratio = front ? M.a0 : M.p;
+        cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
         const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
-        bool refl = ratio * sin_t > 1.;
+        refl = ratio * sin_t > 1.;
+        if constexpr (kTrap) {  // TIR with margin, chords 2 r cos well above 0.01
+            th->tir = !front && ratio * sin_t > 1. + 1e-9 && r * cos_t > 0.0055;
+        }
         if (!refl) {
-            double r0 = (1. - ir) / (1. + ir);
-            r0 = r0 * r0;
+            const double r0 = M.a1;
             const double q = 1. - cos_t;
             const double schlick = r0 + (1. - r0) * (q * ((q * q) * (q * q)));
             refl = schlick > xs_next_01(rng);
         }
-        if (refl) {  // vec3.rs:252-257
-            const double dt = vx * nx + vy * ny + vz * nz;
-            ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2., ndz = vz - (nz * dt) * 2.;
-        } else {  // vec3.rs:259-268
-            const double ct = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
-            const double qx = (vx + nx * ct) * ratio, qy = (vy + ny * ct) * ratio,
-                         qz = (vz + nz * ct) * ratio;
-            const double w = -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
-            ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
-        }
     }
+    double ndx = 0., ndy = 0., ndz = 0.;
+    if (refl) {  // vec3.rs:252-257
+        const double dt = vx * nx + vy * ny + vz * nz;
+        ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2., ndz = vz - (nz * dt) * 2.;
+    }
+    if (kind == RTW_LAMBERTIAN) {  // materials.rs:22-37; near_zero has no abs (vec3.rs:246-250)
+        ndx = nx + ux, ndy = ny + uy, ndz = nz + uz;
+        const bool quirk = ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8;
+        if (quirk) ndx = nx, ndy = ny, ndz = nz;
+        if constexpr (kTrap) {
+            th->lam = !front, th->quirk = quirk;
+            th->ux = ux, th->uy = uy, th->uz = uz;
+            th->a1 = ndx * ndx + ndy * ndy + ndz * ndz;
+        }
+    } else if (kind == RTW_METAL) {  // materials.rs:52-63: reflected + fuzz * u
+        ndx = ndx + ux * M.p, ndy = ndy + uy * M.p, ndz = ndz + uz * M.p;
+    } else if (!refl) {  // vec3.rs:259-268 (its cos is cos_t: the same expression)
+        const double qx = (vx + nx * cos_t) * ratio, qy = (vy + ny * cos_t) * ratio,
+                     qz = (vz + nz * cos_t) * ratio;
+        const double w = -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
+        ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
+    }
+    if (kind != RTW_DIELECTRIC) p.stk.push(static_cast<uint32_t>(best), spill, stride, col);  // attenuation row
     p.ox = px, p.oy = py, p.oz = pz;
     p.dx = ndx, p.dy = ndy, p.dz = ndz;
+    p.prev = best;
     ++p.depth;
     return p.depth >= P.max_depth;  // ray_color(depth >= max) -> black
+}
+
+// Trapped-path fast-forward (rtw_accel.h "Trapped paths"). The path has just
+// scattered inside sphere S (record T) with `rem` segments left before the depth
+// cap. Returns rem if every one of them provably stays inside S -- the sample
+// then ends black, and for a Lambertian trap the RNG has advanced by the rem
+// random_unit_vec draws those bounces make -- or 0 with nothing changed.
+__device__ __forceinline__ uint32_t trap_forward(const double4 T, uint32_t rem, const TrapHint &th,
+                                                 double dx, double dy, double dz, U128 &rng) {
+    const double cap = T.w;
+    if (!(th.h0x * T.x + th.h0y * T.y + th.h0z * T.z < cap)) return 0u;  // the next chord's start
+    if (th.tir) {
+        // the path walks the great circle of S in the plane of h0 and d: all of it
+        // below the cap (|w projected on the plane| < cap) keeps every chord clear
+        double mx = th.h0y * dz - th.h0z * dy, my = th.h0z * dx - th.h0x * dz, mz = th.h0x * dy - th.h0y * dx;
+        const double ml = __builtin_sqrt(mx * mx + my * my + mz * mz);
+        if (!(ml > 1e-3)) return 0u;
+        mx /= ml, my /= ml, mz /= ml;
+        const double wm = T.x * mx + T.y * my + T.z * mz;
+        const double px = T.x - wm * mx, py = T.y - wm * my, pz = T.z - wm * mz;
+        return px * px + py * py + pz * pz < cap * cap && cap > 0. ? rem : 0u;
+    }
+    if (!th.quirk && !(th.a1 >= 1e-9)) return 0u;
+    // end of the next chord: c + r u, or the antipode when near_zero set d = n_in
+    double hx = th.quirk ? -th.h0x : th.ux, hy = th.quirk ? -th.h0y : th.uy, hz = th.quirk ? -th.h0z : th.uz;
+    U128 r2 = rng;
+    for (uint32_t i = 1;; ++i) {
+        if (!(hx * T.x + hy * T.y + hz * T.z < cap)) return 0u;  // end of chord i
+        double vx, vy, vz;
+        random_unit_vec(r2, vx, vy, vz);  // the scatter at the end of segment i
+        if (i >= rem) break;
+        // its direction ~ n_in + u = u - h: near_zero decided with margin, |d|^2 >= 1e-9
+        const double ex = vx - hx, ey = vy - hy, ez = vz - hz;
+        const bool q_yes = ex < -1e-6 && ey < -1e-6 && ez < -1e-6;
+        const bool q_no = ex > 1e-6 || ey > 1e-6 || ez > 1e-6;
+        if (q_yes == q_no) return 0u;
+        if (q_yes) {
+            hx = -hx, hy = -hy, hz = -hz;
+        } else {
+            if (!(ex * ex + ey * ey + ez * ez >= 1e-8)) return 0u;
+            hx = vx, hy = vy, hz = vz;
+        }
+    }
+    rng = r2;
+    return rem;
 }
 
 // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion associates
@@ -494,11 +581,14 @@ __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, 
 // segment loop. `hit(ox, oy, oz, dx, dy, dz, a, bt) -> best` is the Scene::hit
 // strategy. Returns true if the pixel parked: `budget` segments were exceeded at
 // a sample boundary (ps then holds the state to resume from).
-template <class HitFn>
+// With kTrap (drain groups: one path per group, so the branch is uniform) a
+// path trapped inside a sphere is fast-forwarded to its depth cap (trap_forward);
+// `trapped` counts the segments skipped that way.
+template <bool kTrap = false, class HitFn>
 __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView &sv,
                                               uint32_t x, uint32_t y, uint16_t *spill, uint64_t col,
                                               PixelState &ps, uint32_t budget, uint32_t &seg, Stamps &stp,
-                                              HitFn &&hit) {
+                                              HitFn &&hit, uint32_t *trapped = nullptr) {
     const uint32_t n_off = P.n_off;
     if (P.max_depth == 0) {  // every sample is black (no Scene::hit call)
         ps.k = n_off;
@@ -515,10 +605,17 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         ++seg;
         const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
         double bt = 0.;
-        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
         STAMP(1);
         double lr, lg, lb;
-        const bool done = shade(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp);
+        TrapHint th;
+        bool done = shade<kTrap>(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp, &th);
+        if constexpr (kTrap) {
+            if (!done && (th.lam || th.tir)) {
+                const uint32_t k = trap_forward(P.trap[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
+                if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
+            }
+        }
         STAMP(3);  // 3: hit record + scatter / sky
         if (done) {
             fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
@@ -589,8 +686,36 @@ struct Seg32 {
 
 // Counters kept per lane, atomically added at the end of a kernel.
 struct Tally {
-    uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0, parked = 0, witer = 0;
+    uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0, parked = 0, witer = 0, inside = 0,
+             trap = 0;
 };
+
+// Inside cut (rtw_accel.h): the segment starts inside `prev`, the sphere it last
+// hit, and leaves it through the far root -- then only prev's list can come
+// nearer. Returns true with the scan's (best, bt) if the cut applies.
+__device__ __forceinline__ bool inside_hit(const double4 *__restrict__ sph, const ShadeRec *__restrict__ shd,
+                                           const uint16_t *__restrict__ nbr, int prev, double ox, double oy,
+                                           double oz, double dx, double dy, double dz, double a, int &best,
+                                           double &bt, Tally &tl, bool count = true) {
+    if (prev < 0) return false;
+    const uint32_t info = shd[prev].nbr;
+    if (info == rtw_accel::kNbrNone) return false;
+    const double4 S = sph[prev];
+    double t;
+    if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t)) return false;
+    const uint32_t n = info & 0xffu;
+    if (count) tl.inside += 1u, tl.ntest += 1u + n;
+    best = prev, bt = t;
+    const uint16_t *l = nbr + (info >> 8);
+    for (uint32_t j = 0; j < n; ++j) {
+        const uint32_t i = l[j];
+        const double4 T = sph[i];
+        if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w, t) &&
+            rtw_accel::better(t, i, bt, best))
+            bt = t, best = static_cast<int>(i);
+    }
+    return true;
+}
 
 // The scan: every sphere in index order (first = lane's sub-range start, step =
 // sphere stride for cooperative groups); pass 1 = f32 filter on wave-uniform
@@ -633,13 +758,16 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 // Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
 // exact candidates, the cut check; anything unproven falls back to the scan.
 template <bool kLdsStack = false>
-__device__ __forceinline__ int bvh_hit(const KParams &P, const double4 *__restrict__ sph,
-                                       const float4 *__restrict__ nodes,
-                                       const float4 *__restrict__ leaves, double ox, double oy,
-                                       double oz, double dx, double dy, double dz, double a,
+__device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
+                                       double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr) {
-    const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
+    const double4 *__restrict__ sph = sv.sph;
+    const float4 *__restrict__ nodes = sv.nodes;
+    const float4 *__restrict__ leaves = sv.leaves;
     int best = -1;
+    if (P.inside_cursor && inside_hit(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl))
+        return best;
+    const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
     bool brute = !g.fast;
     if (g.fast) {
         for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
@@ -709,11 +837,13 @@ __device__ __forceinline__ void flush_tally(const KParams &P, const Tally &tl, b
 #endif
     if (tl.nbrute) atomicAdd(&P.counters[5], static_cast<unsigned long long>(tl.nbrute));
     if (tl.parked) atomicAdd(&P.counters[6], static_cast<unsigned long long>(tl.parked));
+    if (tl.inside) atomicAdd(&P.counters[8], static_cast<unsigned long long>(tl.inside));
+    if (tl.trap) atomicAdd(&P.counters[9], static_cast<unsigned long long>(tl.trap));
 }
 
 template <bool kLds, int kMode>
 __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds) {
-    SceneView v{P.sph, P.shade, P.nodes, P.leaves};
+    SceneView v{P.sph, P.shade, P.nodes, P.leaves, P.nbr};
     if (kLds) {
         const uint32_t n = P.n_sph;
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = P.sph[i];
@@ -724,6 +854,9 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
             const uint32_t nn = rtw_accel::kNodeF4 * P.n_node, nl = 2u * P.n_leaf;
             for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lf[i] = P.nodes[i];
             for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) lf[nn + i] = P.leaves[i];
+            uint16_t *lnb = reinterpret_cast<uint16_t *>(lf + nn + nl);
+            for (uint32_t i = threadIdx.x; i < P.n_nbr; i += blockDim.x) lnb[i] = P.nbr[i];
+            v.nbr = lnb;
         }
         __syncthreads();
         v.sph = lds;
@@ -741,7 +874,6 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
     const double4 *sph = sv.sph;
-    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
 
     const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
     const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
@@ -757,9 +889,9 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
         ps.ar = ps.ag = ps.ab = 0.;
         const uint64_t pix = static_cast<uint64_t>(lr) * P.W + x;  // spill column
         auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
-                       double &bt) -> int {
+                       int prev, double &bt) -> int {
             if constexpr (kMode == kBvh) {
-                return bvh_hit(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp);
+                return bvh_hit(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp);
             } else {
                 const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
                 return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -888,11 +1020,14 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
 #pragma unroll
         for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u)];
     }
-    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
-        const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
         int best = -1;
         bt = 0.;
+        // inside cut: every lane of the group holds the same path, so the branch
+        // is group-uniform and the lanes run the (short) list redundantly
+        if (inside_hit(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl, sub == 0)) return best;
+        const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
         STAMP(0);  // coop: loop back + segment setup (Seg32)
         if (rec_in_regs) {
             uint32_t mask = 0;
@@ -934,8 +1069,9 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         group_min<kG>(bt, best);
         return best;
     };
-    uint32_t s = 0;
-    trace_samples(P, sv, q.x, y, P.spill_b, col, ps, 0xffffffffu, s, stp, hit);
+    uint32_t s = 0, trapped = 0;
+    trace_samples<true>(P, sv, q.x, y, P.spill_b, col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    if (sub == 0) tl.trap += trapped;
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
         if (P.diag) {
@@ -1006,8 +1142,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
                 ++segs;
                 const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
                 double bt = 0.;
-                const int best = bvh_hit(P, sv.sph, sv.nodes, sv.leaves, p.ox, p.oy, p.oz, p.dx, p.dy,
-                                         p.dz, a, bt, tl, stp);
+                const int best = bvh_hit(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp);
                 if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
                 double cr, cg, cb;
                 shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
@@ -1093,7 +1228,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
     // pass-1 records after the scene view: after the leaves (BVH) or the shading records
     float4 *filt_lds = reinterpret_cast<float4 *>(reinterpret_cast<ShadeRec *>(lds_sph + P.n_sph) + P.n_sph);
-    if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf;
+    if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf + nbr_f4(P.n_nbr);
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
     // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
     // read and written once per sample) and the BVH walk scratch (kScratch u16
@@ -1101,7 +1236,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
     uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);
     const double4 *sph = sv.sph;
-    const float4 *nodes = sv.nodes, *leaves = sv.leaves;
     Tally tl;
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
@@ -1112,11 +1246,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
 
     Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
-    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
+    auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true>(P, sph, nodes, leaves, ox, oy, oz, dx, dy, dz, a, bt, tl, stp,
-                                 lane_stk + threadIdx.x);
+            return bvh_hit<true>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -1187,7 +1320,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
             double bt = 0.;
             STAMP(0);  // 0: loop top, refill
-            const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, bt);
+            const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
             STAMP(1);  // 1: hit tail (exact candidates, cut check)
             double cr, cg, cb;
             const bool ended = shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb, stp);
@@ -1358,6 +1491,9 @@ struct rtw_session {
     double4 *d_sph = nullptr;
     float4 *d_filt = nullptr;
     ShadeRec *d_shade = nullptr;
+    uint16_t *d_nbr = nullptr;  // inside-cut lists
+    uint32_t n_nbr = 0;
+    double4 *d_trap = nullptr;  // per-sphere trapped-path records
     uint4 *d_jump = nullptr;
     unsigned long long *d_counters = nullptr;
     uint16_t *d_spill = nullptr;
@@ -1420,10 +1556,10 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
     dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_shade);
+    dev_free(s->d_shade), dev_free(s->d_nbr), dev_free(s->d_trap);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     s->d_sph = nullptr, s->d_filt = nullptr;
-    s->d_shade = nullptr;
+    s->d_shade = nullptr, s->d_nbr = nullptr, s->n_nbr = 0, s->d_trap = nullptr;
     s->d_nodes = nullptr, s->d_leaves = nullptr, s->d_always = nullptr;
     s->has_bvh = false, s->scene_set = false;
     s->n_node = s->n_leaf = s->n_always = 0;
@@ -1448,8 +1584,53 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         R.r = rad;
         R.a0 = M.albedo[0], R.a1 = M.albedo[1], R.a2 = M.albedo[2];
         R.p = M.kind == RTW_METAL ? M.fuzz : M.kind == RTW_DIELECTRIC ? M.ir : 0.;
-        R.kind = M.kind, R._pad = 0;
+        R.kind = M.kind, R.nbr = rtw_accel::kNbrNone;
+        if (M.kind == RTW_DIELECTRIC) {
+            // the refraction ratio 1/ir and reflectance's r0*r0 (materials.rs:75-89),
+            // with the reference's IEEE operations (attenuation is 1: no albedo row)
+            const double ir = M.ir;
+            double r0 = (1. - ir) / (1. + ir);
+            r0 = r0 * r0;
+            R.a0 = 1. / ir, R.a1 = r0, R.a2 = 0.;
+        }
     }
+    // inside-cut lists (rtw_accel.h): per sphere the spheres that can come nearer
+    // than its far root for a ray starting inside it
+    std::vector<uint16_t> nbr_ids;
+    {
+        std::vector<double> cen(3 * static_cast<size_t>(n)), rad(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            for (int k = 0; k < 3; ++k) cen[3 * i + k] = sp[i].center[k];
+            rad[i] = sp[i].radius;
+        }
+        // spheres that can trap a path (rtw_accel.h "Trapped paths"): Lambertian
+        // with a finite albedo >= +0 (the black product then keeps its bits), or
+        // Dielectric with a finite ir (total internal reflection)
+        std::vector<uint8_t> trap_ok(n, 0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const rtw_material &M = m[sp[i].mat];
+            bool ok = false;
+            if (M.kind == RTW_LAMBERTIAN) {
+                ok = true;
+                for (int k = 0; k < 3; ++k)
+                    ok = ok && std::isfinite(M.albedo[k]) && !std::signbit(M.albedo[k]);
+            } else if (M.kind == RTW_DIELECTRIC) {
+                ok = std::isfinite(M.ir) && M.ir > 0.;
+            }
+            trap_ok[i] = ok ? 1 : 0;
+        }
+        std::vector<uint32_t> info;
+        std::vector<rtw_accel::TrapRec> traps;
+        rtw_accel::build_inside(cen.data(), rad.data(), n, info, nbr_ids, trap_ok.data(), &traps);
+        for (uint32_t i = 0; i < n; ++i) sh[i].nbr = info[i];
+        static_assert(sizeof(rtw_accel::TrapRec) == sizeof(double4), "TrapRec layout");
+        HIPCHECK(hipMalloc(&s->d_trap, (n ? n : 1) * sizeof(double4)));
+        if (n) HIPCHECK(hipMemcpy(s->d_trap, traps.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+    }
+    HIPCHECK(hipMalloc(&s->d_nbr, (nbr_ids.size() + 8) * sizeof(uint16_t)));
+    if (!nbr_ids.empty())
+        HIPCHECK(hipMemcpy(s->d_nbr, nbr_ids.data(), nbr_ids.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    s->n_nbr = static_cast<uint32_t>(nbr_ids.size());
     HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
     HIPCHECK(hipMalloc(&s->d_filt, f.size() * sizeof(float4)));
     HIPCHECK(hipMalloc(&s->d_shade, sh.size() * sizeof(ShadeRec)));
@@ -1556,6 +1737,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.sph = s->d_sph;
     P.filt = s->d_filt;
     P.shade = s->d_shade;
+    P.nbr = s->d_nbr;
+    P.n_nbr = s->n_nbr;
+    P.trap = s->d_trap;
+    // the inside cut costs one-lane-per-pixel waves more than it saves (the wave
+    // still walks for its other lanes): drain groups only, RTW_INSIDE=1 for A/B
+    P.inside_cursor = 0;
+    if (const char *e = std::getenv("RTW_INSIDE")) P.inside_cursor = static_cast<uint32_t>(std::atoi(e));
     P.jump = s->d_jump;
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
@@ -1662,7 +1850,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     // phase 1: persistent per-lane refill (default) or one tile per workgroup (RTW_PERSIST=0)
     bool persist = true;
     if (const char *e = std::getenv("RTW_PERSIST")) persist = std::atoi(e) != 0;
-    size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh);
+    size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh, P.n_nbr);
     if (persist) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);  // pass-1 records (coop groups)
     const bool use_lds = lds <= kLdsCap;
     if (!use_lds) lds = 0;
@@ -1688,7 +1876,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
-            const size_t lds_p = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true);
+            const size_t lds_p = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true, P.n_nbr);
             if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, g1, dim3(kBlock), lds_p, st, P);
             else hipLaunchKernelGGL(rtw_cost_probe<false>, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_bucket, gt, dim3(kBlock), 0, st, P);
@@ -1796,6 +1984,8 @@ void collect(rtw_session *s) {
     s->last.node_visits = c[4];
     s->last.brute_segments = c[5];
     s->last.parked_pixels = c[6];
+    s->last.inside_segments = c[8];
+    s->last.trap_segments = c[9];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->pending = false;
@@ -1872,7 +2062,7 @@ int rtw_session_destroy(rtw_session *s) {
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
     dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_shade);
+    dev_free(s->d_shade), dev_free(s->d_nbr), dev_free(s->d_trap);
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);

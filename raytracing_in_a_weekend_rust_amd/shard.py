@@ -1,4 +1,9 @@
-"""Row-cyclic image sharding over ranks.
+"""Multi-GPU work split: frames per rank, or one frame's rows.
+
+Weak scaling (bench.py default): an N-rank job renders N frames of the workload,
+one whole frame per rank (frame_seed); no data-path collective.
+
+Row-cyclic sharding of one frame (bench.py --scaling strong, BASELINE configs[3]):
 
 Pixels are independent and each pixel's RNG stream depends only on its global
 index (copy_reset chain, camera.rs:269-272), so any row partition reproduces the
@@ -8,6 +13,14 @@ of the row tiles (RCCL all_gather over xGMI on GPUs, gloo in CPU tests),
 followed by an un-permute on the receiving rank.
 """
 from __future__ import annotations
+
+
+def frame_seed(seed: int, frame: int) -> int:
+    """Render seed of frame `frame` of a multi-frame job. The reference seeds every
+    render from the wall clock in ms (random.rs:16-22, camera.rs:255), so renders
+    made one after another see consecutive seeds; frame 0 is the single-GPU
+    workload itself."""
+    return (seed + frame) % (1 << 128)
 
 
 def rows_of(rank: int, world: int, height: int):

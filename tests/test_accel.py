@@ -25,6 +25,11 @@ SCENES = [
     ("random:40", 1, 20000),
     ("random:300", 2, 10000),
     ("random:700", 3, 5000),
+    # near-tangent / overlapping clusters at offsets up to 2^13: inside-cut margins
+    ("touch:30", 1, 10000),
+    ("touch:100", 2, 10000),
+    ("touch:200", 13, 10000),
+    ("touch:150", 7, 10000),
 ]
 
 
@@ -47,6 +52,8 @@ def test_walk_matches_scan(exe, scene, seed, paths):
         # the walk replaces the 486-sphere scan by ~20 node/leaf tests
         assert r["visits_per_walk"] < 40, r
         assert r["fallbacks"] + r["overflows"] < r["rays"] // 1000, r
+    if scene == "complex" or scene.startswith("touch:"):
+        assert r["inside_cuts"] > r["rays"] // 10, r  # the inside cut was exercised
 
 
 def test_ineligible_scene_reports_no_bvh(exe):

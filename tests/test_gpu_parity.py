@@ -288,3 +288,34 @@ def test_deep_paths_use_spill_levels():
         ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, 31)
         assert_same(fb, ref, st, seg)
         assert st.segments == st.samples * depth  # nothing ever escapes
+
+
+@pytest.mark.parametrize("budget", ["0.01", "0"])
+def test_trapped_paths_fast_forward(monkeypatch, budget):
+    """Scenes that trap paths (rtw_accel.h "Trapped paths"): Lambertian spheres
+    hovering within 0.01 of a big Lambertian ground (rays slip inside through the
+    skipped near root), an overlapping Lambertian pair (neighbour half-space), a
+    glass sphere (total internal reflection) and a small glass sphere inside a big
+    one. With every pixel parked (budget 0.01) the drain groups fast-forward the
+    trapped samples; the image, the segment count and the RNG streams after them
+    must match the oracle bit-for-bit."""
+    monkeypatch.setenv("RTW_BUDGET_X", budget)
+    world = rtw.SceneBuilder()
+    world.add(rtw.Sphere.new_world_obj(0., -100., 0., 100., rtw.Lambertian((0.6, 0.6, 0.5))))
+    for i, gap in enumerate((0.001, 0.004, 0.0095, 0.02)):
+        world.add(rtw.Sphere.new_world_obj(-1.5 + i, 0.3 + gap + (i * i) * 1e-3, -0.5, 0.3,
+                                           rtw.Lambertian((0.3 + 0.1 * i, 0.5, 0.7))))
+    world.add(rtw.Sphere.new_world_obj(-0.6, 0.45, -1.6, 0.45, rtw.Lambertian((0.8, 0.3, 0.2))))
+    world.add(rtw.Sphere.new_world_obj(0.1, 0.45, -1.6, 0.45, rtw.Lambertian((0.2, 0.8, 0.3))))  # overlaps
+    world.add(rtw.Sphere.new_world_obj(1.3, 0.6, -1.5, 0.6, rtw.Dielectric(1.5)))
+    world.add(rtw.Sphere.new_world_obj(1.3, 0.6, -1.5, 0.2, rtw.Dielectric(2.4)))  # glass in glass
+    world.add(rtw.Sphere.new_world_obj(-2.4, 0.5, -2.2, 0.5, rtw.Metal((0.8, 0.8, 0.8), 0.3)))
+    scene = world.build()
+    sph, n, mt, nm = scene.flatten()
+    cam = rtw.Camera.new(40, 64, 50, 1.0, 40.0, (0., 1.2, 3.5), (0., 0.3, -1.), (0., 1., 0.), 0.3, 4.0)
+    fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, 3, 1234)
+    ref, seg = orc.render(cam.raw, sph, n, mt, nm, 3, 1234)
+    assert_same(fb, ref, st, seg)
+    if budget == "0.01":
+        assert st.parked_pixels == 40 * 64
+        assert st.trap_segments > 0

@@ -1,7 +1,10 @@
-"""Multi-rank path on the CPU: world_size 2 over gloo. Each rank renders its
-row-cyclic shard (here with the oracle, the GPU kernel's checker), the tiles are
-all-gathered and un-permuted by the same code bench.py uses, and the result must
-equal the unsharded image bit-for-bit."""
+"""Multi-rank paths on the CPU over gloo (world_size 2 and 3), with the oracle (the
+GPU kernel's checker) as the renderer:
+- strong (bench.py --scaling strong): each rank renders its row-cyclic shard, the
+  tiles are all-gathered and un-permuted by the same code bench.py uses, and the
+  result equals the unsharded image bit-for-bit;
+- weak (bench.py default): rank r renders frame r of the job at
+  shard.frame_seed(SEED, r), frame 0 being the single-GPU workload."""
 import os
 import socket
 
@@ -66,3 +69,32 @@ def test_shard_rows_cover_image_once():
         assert sorted(seen) == list(range(675))
         src, dst = shard.unpermute_index(world, 675)
         assert sorted(dst.tolist()) == list(range(675))
+
+
+def _frame_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle_ctypes as orc
+    cam, sph, mat, n = _scene()
+    fb, _ = orc.render(cam, sph, n, mat, n, S, shard.frame_seed(SEED, rank), nthreads=2)
+    frame = torch.from_numpy(fb)
+    frames = [torch.zeros_like(frame) for _ in range(world)]
+    dist.all_gather(frames, frame)  # the test's check only: the bench's weak path has no collective
+    if rank == 0:
+        np.save(out, torch.stack(frames).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_frame_per_rank_weak_scaling(tmp_path):
+    from oracle import oracle_ctypes as orc
+    world = 2
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_frame_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    cam, sph, mat, n = _scene()
+    assert shard.frame_seed(SEED, 0) == SEED
+    for f in range(world):
+        ref, _ = orc.render(cam, sph, n, mat, n, S, shard.frame_seed(SEED, f), nthreads=2)
+        assert np.array_equal(got[f], ref)
+    assert not np.array_equal(got[0], got[1])  # independent frames, not replicas

@@ -46,6 +46,8 @@ struct Scene {
     uint32_t n = 0;
     Bvh bvh;
     bool bvh_ok = false;
+    std::vector<uint32_t> nbr_info;  // inside-cut lists (build_inside)
+    std::vector<uint16_t> nbr_ids;
 };
 
 struct Hit {
@@ -68,13 +70,32 @@ static Hit brute(const Scene &S, const double o[3], const double d[3]) {
 
 struct Counts {
     uint64_t rays = 0, walked = 0, visits = 0, max_visits = 0, cands = 0, fallbacks = 0,
-             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0;
+             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0, inside = 0;
 };
 
-// The kernel's accelerated Scene::hit, host-side.
-static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k) {
+// The kernel's accelerated Scene::hit, host-side. `prev` = the sphere the path
+// last hit (-1: none): the inside cut is tried first, as on the device.
+static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k, int prev) {
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     Hit h;
+    if (prev >= 0 && S.nbr_info[prev] != kNbrNone) {
+        const uint32_t s = static_cast<uint32_t>(prev);
+        double t;
+        if (inside_far(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * s], S.c[3 * s + 1], S.c[3 * s + 2],
+                       S.rr[s], t)) {
+            ++k.inside;
+            h.idx = prev, h.t = t;
+            const uint32_t info = S.nbr_info[s];
+            for (uint32_t j = 0; j < (info & 0xffu); ++j) {
+                const uint32_t i = S.nbr_ids[(info >> 8) + j];
+                if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
+                                   S.c[3 * i + 2], S.rr[i], t) &&
+                    better(t, i, h.t, h.idx))
+                    h.idx = static_cast<int>(i), h.t = t;
+            }
+            return h;
+        }
+    }
     for (uint32_t i : S.bvh.always) {
         double t;
         if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
@@ -124,10 +145,11 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
     return h;
 }
 
-static void check(const Scene &S, const double o[3], const double d[3], Counts &k, Hit *out) {
+static void check(const Scene &S, const double o[3], const double d[3], Counts &k, Hit *out,
+                  int prev = -1) {
     ++k.rays;
     const Hit b = brute(S, o, d);
-    const Hit x = accel(S, o, d, k);
+    const Hit x = accel(S, o, d, k, prev);
     if (b.idx != x.idx || (b.idx >= 0 && std::memcmp(&b.t, &x.t, 8) != 0)) {
         if (k.mismatches < 10)
             fprintf(stderr, "MISMATCH o=(%.17g,%.17g,%.17g) d=(%.17g,%.17g,%.17g) brute=%d/%.17g accel=%d/%.17g\n",
@@ -147,6 +169,7 @@ static void finish_scene(Scene &S) {
         S.r2p[i] = filter_r2p(&S.c[3 * i], S.rr[i]);
     }
     S.bvh_ok = build(S.c.data(), S.r.data(), S.r2p.data(), S.n, S.bvh);
+    build_inside(S.c.data(), S.r.data(), S.n, S.nbr_info, S.nbr_ids);
 }
 
 int main(int argc, char **argv) {
@@ -181,6 +204,32 @@ int main(int argc, char **argv) {
             S.r.push_back(r);
         }
         from[0] = 9, from[1] = 3, from[2] = 7;
+    } else if (name.rfind("touch:", 0) == 0) {
+        // near-tangent clusters: each sphere placed against an earlier one with a
+        // gap of +-2^-k of the radii (k up to 60: overlapping, touching, just
+        // apart), some nested, at a random offset up to 1e4 (inside-cut margins)
+        const uint32_t K = static_cast<uint32_t>(std::atoi(name.c_str() + 6));
+        const double off = std::ldexp(1., static_cast<int>(seed % 14));
+        for (uint32_t i = 0; i < K; ++i) {
+            double r = 0.05 + 0.5 * rng.u01();
+            double cc[3] = {off + 4 * rng.sym(), 2 * rng.sym(), off + 4 * rng.sym()};
+            if (i > 0 && rng.u01() < 0.8) {
+                const uint32_t j = static_cast<uint32_t>(rng.next() % i);
+                double v[3], vl;
+                do {
+                    v[0] = rng.sym(), v[1] = rng.sym(), v[2] = rng.sym();
+                    vl = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                } while (vl > 1. || vl < 1e-3);
+                const double rj = std::fabs(S.r[j]);
+                const double gap = std::ldexp(rng.sym(), -static_cast<int>(rng.next() % 61)) * (r + rj);
+                const double dist = rng.u01() < 0.1 ? std::fabs(rj - r) * rng.u01() : rj + r + gap;
+                for (int k2 = 0; k2 < 3; ++k2) cc[k2] = S.c[3 * j + k2] + v[k2] / vl * dist;
+            }
+            S.c.insert(S.c.end(), {cc[0], cc[1], cc[2]});
+            S.r.push_back(r);
+        }
+        from[0] = off + 9, from[1] = 3, from[2] = off + 7;
+        to[0] = off, to[2] = off;
     } else {
         rtw_camera cam;
         std::vector<rtw_sphere> sp(4096);
@@ -209,10 +258,12 @@ int main(int argc, char **argv) {
         double o[3] = {from[0] + 0.05 * rng.sym(), from[1] + 0.05 * rng.sym(), from[2] + 0.05 * rng.sym()};
         double d[3];
         for (int j = 0; j < 3; ++j) d[j] = (to[j] - from[j]) + 3.0 * rng.sym() * (j == 1 ? 0.6 : 1.0);
+        int prev = -1;
         for (int depth = 0; depth < 50; ++depth) {
             Hit h;
-            check(S, o, d, k, &h);
+            check(S, o, d, k, &h, prev);
             if (h.idx < 0) break;
+            prev = h.idx;
             const uint32_t i = static_cast<uint32_t>(h.idx);
             double pnt[3], n[3];
             for (int j = 0; j < 3; ++j) pnt[j] = d[j] * h.t + o[j];
@@ -242,7 +293,7 @@ int main(int argc, char **argv) {
         double d[3] = {rng.sym(), rng.sym(), rng.sym()};
         const double sc = std::exp(12 * rng.sym());  // unnormalised directions, many scales
         for (double &x : d) x *= sc;
-        check(S, o, d, k, nullptr);
+        check(S, o, d, k, nullptr, S.n ? static_cast<int>(rng.next() % S.n) : -1);
     }
     // 3. near-tangent rays to random spheres (silhouettes), from outside and on-surface
     for (uint64_t p = 0; p < npaths && S.n; ++p) {
@@ -265,17 +316,43 @@ int main(int argc, char **argv) {
             o[j] = S.c[3 * i + j] + q[j] / ql * off - w[j] * back;
             d[j] = w[j] * std::exp(4 * rng.sym());
         }
-        check(S, o, d, k, nullptr);
+        check(S, o, d, k, nullptr, static_cast<int>(i));
+    }
+    // 4. rays from inside a sphere (interior points, and surface points with an
+    // inward direction: trapped-ray bounces), hinted with that sphere
+    for (uint64_t p = 0; p < npaths && S.n; ++p) {
+        const uint32_t i = static_cast<uint32_t>(rng.next() % S.n);
+        const double R = std::fabs(S.r[i]);
+        if (!(R < 1e6)) continue;
+        double v[3], vl;
+        do {
+            v[0] = rng.sym(), v[1] = rng.sym(), v[2] = rng.sym();
+            vl = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        } while (vl > 1. || vl < 1e-3);
+        const double u = rng.u01();
+        const double rad = u < 0.5 ? R : R * (u < 0.75 ? vl : 1. + std::ldexp(rng.sym(), -30));
+        double o[3], d[3];
+        for (int j = 0; j < 3; ++j) o[j] = S.c[3 * i + j] + v[j] / vl * rad;
+        double w[3], wl;
+        do {
+            w[0] = rng.sym(), w[1] = rng.sym(), w[2] = rng.sym();
+            wl = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+        } while (wl > 1. || wl < 1e-3);
+        // inward: -n + unit (Lambertian from the inner face), or any direction
+        const double in = rng.u01() < 0.7 ? -1. : 0.;
+        const double sc = std::exp(3 * rng.sym());
+        for (int j = 0; j < 3; ++j) d[j] = (in * v[j] / vl + w[j] / wl) * sc;
+        check(S, o, d, k, nullptr, static_cast<int>(i));
     }
     printf("{\"scene\": \"%s\", \"bvh\": true, \"n\": %u, \"always\": %zu, \"inner\": %u, \"depth\": %u, "
            "\"rays\": %llu, \"hits\": %llu, \"walked\": %llu, \"visits_per_walk\": %.3f, \"max_visits\": %llu, "
            "\"cands_per_walk\": %.3f, \"fallbacks\": %llu, \"overflows\": %llu, \"not_walkable\": %llu, "
-           "\"mismatches\": %llu}\n",
+           "\"inside_cuts\": %llu, \"mismatches\": %llu}\n",
            name.c_str(), S.n, S.bvh.always.size(), S.bvh.n_node, S.bvh.depth, (unsigned long long)k.rays,
            (unsigned long long)k.hits, (unsigned long long)k.walked,
            k.walked ? double(k.visits) / k.walked : 0., (unsigned long long)k.max_visits,
            k.walked ? double(k.cands) / k.walked : 0., (unsigned long long)k.fallbacks,
            (unsigned long long)k.overflows, (unsigned long long)k.not_walkable,
-           (unsigned long long)k.mismatches);
+           (unsigned long long)k.inside, (unsigned long long)k.mismatches);
     return k.mismatches ? 1 : 0;
 }

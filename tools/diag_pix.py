@@ -10,12 +10,15 @@ import raytracing_in_a_weekend_rust_amd as rtw
 
 os.environ["RTW_DIAG"] = "1"
 W, H, S = 1200, 675, int(sys.argv[1]) if len(sys.argv) > 1 else 23
+NSH, RSH = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (1, 0)  # shard N:r
 seed = rtw.DEFAULT_SEED
 cam, sph, n, mt, nm = rtw.builtin_scene("complex", seed, H, W, 50)
 sess = rtw.Session(0)
 sess.set_scene(sph, n, mt, nm)
 fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0")
-sess.render(cam.raw, S, seed, fb.data_ptr())
+from raytracing_in_a_weekend_rust_amd import shard as _sh  # noqa: E402
+rb, rstep, H = _sh.rows_of(RSH, NSH, H)  # H: this shard's rows from here on
+sess.render(cam.raw, S, seed, fb.data_ptr(), shard=(rb, rstep, H))
 st = sess.stats()
 d, t0 = sess.diag(W * H)
 seg = d[:, 0].astype(np.float64) / (S * S)
