@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Per-launch instruction counts of the persistent render kernel from a rocprofv3
 --pmc pass (SQ_INSTS_* count wave-level instructions). The bulk of the launch is
-VALU-issue bound: one wave64 VALU instruction occupies a SIMD for 4 cycles, so
-issue utilisation = VALU x 4 / (SIMDs x clock x kernel time).
-Usage: pmc_insts.py OUTDIR  (expects OUTDIR/pmc_insts)."""
+limited by VALU issue and latency: on gfx950 a wave64 f32/int VALU instruction
+occupies the SIMD for 2 cycles, an f64 one for 4 (bench.py valu_issue).
+Usage: pmc_insts.py OUTDIR [PASS]  (expects OUTDIR/PASS, default pmc_insts)."""
 import csv
 import glob
 import json
@@ -15,8 +15,9 @@ KERNEL = "rtw_render_persist"
 
 def main():
     out = sys.argv[1]
+    sub = sys.argv[2] if len(sys.argv) > 2 else "pmc_insts"
     acc, launches = {}, {}
-    for f in glob.glob(os.path.join(out, "pmc_insts", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(out, sub, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if KERNEL in row["Kernel_Name"]:
