@@ -1917,17 +1917,23 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, pblock, lds));
         if (per_cu < 1) per_cu = 1;
         grid_p = static_cast<uint32_t>(per_cu) * static_cast<uint32_t>(s->n_cu > 0 ? s->n_cu : 256);
-        const uint64_t need_blocks = (npix + pblock - 1) / pblock;
-        if (grid_p > need_blocks) grid_p = static_cast<uint32_t>(need_blocks);
-        // heavy waves per workgroup (RTW_HEAVY, default 1): raised priority, parked pixels only
-        uint32_t heavy = kHeavyPerBlock;
-        if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
+        // every CU gets a workgroup even when the shard has fewer pixels than the
+        // launch has lanes: pixels then spread over all CUs (shorter per-lane
+        // iterations), and the waves left without a pixel drain the park queue
+        // heavy waves per workgroup (RTW_HEAVY, default 2): raised priority, parked
+        // pixels only. A shard with fewer pixels than cursor lanes (strong scaling
+        // at N >= 8) leaves whole waves without a pixel from the start: those drain
+        // the park queue, so no wave is reserved and no pixel is parked for being
+        // late (dry-cursor parking off) -- measured 86 vs 93 ms per rank at N=8.
         const uint32_t wpb = static_cast<uint32_t>(pblock) / 64u;
+        const bool small_shard = npix < static_cast<uint64_t>(grid_p) * (wpb - kHeavyPerBlock) * 64u;
+        uint32_t heavy = small_shard ? 0u : kHeavyPerBlock;
+        if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
         P.n_cursor_waves = grid_p * (wpb - heavy);
         P.rate_k = 16, P.rate_x = 16;
-        P.tail_segs = kTailSegs;
+        P.tail_segs = small_shard ? 0xffffffffu : kTailSegs;
         if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
