@@ -1,0 +1,36 @@
+"""Developer tool: A/B of library builds on one GPU box, interleaved.
+
+Runs bench.py (no CPU leg) once per library per round, alternating, with RTW_LIB
+pointing at each build, and prints every ms_per_step and the per-library mean.
+usage: python tools/libab.py ROUNDS LIB [LIB ...]
+"""
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    rounds = int(sys.argv[1])
+    libs = sys.argv[2:]
+    res = {lib: [] for lib in libs}
+    for r in range(rounds):
+        for lib in libs:
+            env = dict(os.environ, RTW_LIB=os.path.abspath(lib))
+            p = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--steps", "3", "--warmup", "1",
+                                "--cpu-baseline", "0"], env=env, capture_output=True, text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if p.returncode != 0 or not line:
+                print(f"{lib}: failed rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
+                sys.exit(1)
+            ms = json.loads(line[-1])["ms_per_step"]
+            res[lib].append(ms)
+            print(f"round {r} {os.path.basename(lib)}: {ms:.2f} ms", flush=True)
+    for lib, v in res.items():
+        print(f"{os.path.basename(lib)}: mean {sum(v) / len(v):.2f} ms  {['%.2f' % x for x in v]}")
+
+
+if __name__ == "__main__":
+    main()
