@@ -114,8 +114,7 @@ struct KParams {
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
     uint32_t tail_segs, _pad5;  // once the cursor is dry: park pixels with more estimated work left
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
-    uint32_t n_nbr;             // inside-cut list entries
-    uint32_t inside_cursor;     // 1: one-lane-per-pixel paths try the inside cut (drain groups always do)
+    uint32_t n_nbr, _pad6;      // inside-cut list entries
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -765,8 +764,6 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
     const float4 *__restrict__ nodes = sv.nodes;
     const float4 *__restrict__ leaves = sv.leaves;
     int best = -1;
-    if (P.inside_cursor && inside_hit(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl))
-        return best;
     const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
     bool brute = !g.fast;
     if (g.fast) {
@@ -1104,7 +1101,7 @@ __device__ __forceinline__ const float4 *stage_filt(const KParams &P, float4 *lf
 // (a chain started late ends late), the cheapest tiles fill the drain, and lanes
 // refilled together get neighbouring pixels (coherent rays).
 constexpr uint32_t kProbeSamples = 2;
-constexpr uint32_t kHotSegs = 2 * 10;  // probe segments: >= 10 per sample
+constexpr uint32_t kHotSegs = kProbeSamples * 10;  // probe segments: >= 10 per sample
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kOrderTile = 8;
 struct TileGrid {
@@ -1745,10 +1742,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.nbr = s->d_nbr;
     P.n_nbr = s->n_nbr;
     P.trap = s->d_trap;
-    // the inside cut costs one-lane-per-pixel waves more than it saves (the wave
-    // still walks for its other lanes): drain groups only, RTW_INSIDE=1 for A/B
-    P.inside_cursor = 0;
-    if (const char *e = std::getenv("RTW_INSIDE")) P.inside_cursor = static_cast<uint32_t>(std::atoi(e));
     P.jump = s->d_jump;
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
