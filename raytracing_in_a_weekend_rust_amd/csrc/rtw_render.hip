@@ -114,7 +114,8 @@ struct KParams {
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
     uint32_t tail_segs, _pad5;  // once the cursor is dry: park pixels with more estimated work left
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
-    uint32_t n_nbr, _pad6;      // inside-cut list entries
+    uint32_t n_nbr;             // inside-cut list entries
+    uint32_t s_magic;           // ceil(2^32 / s) for k / s by a multiply-high (s <= 1625), else 0
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -378,7 +379,9 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
     if (P.s == 0) {
         offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
     } else {
-        const uint32_t ly = k / P.s, lx = k - ly * P.s;
+        // k / s exactly by a multiply-high when k e < 2^32 (e = m s - 2^32 < s, k < s^2):
+        // s^3 <= 2^32 (host: s <= 1625)
+        const uint32_t ly = P.s_magic ? __umulhi(k, P.s_magic) : k / P.s, lx = k - ly * P.s;
         const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
         offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
         offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
@@ -628,8 +631,8 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
 }
 
 __device__ __forceinline__ void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
-                                            const PixelState &ps) {
-    if (P.pixels_done) atomicAdd(P.pixels_done, 1u);
+                                            const PixelState &ps, bool count = true) {
+    if (count && P.pixels_done) atomicAdd(P.pixels_done, 1u);
     const double nf = static_cast<double>(P.n_off);
     double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
     o[0] = ps.ar / nf;
@@ -1339,11 +1342,17 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                                        static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
+                {  // one completion-count atomic per wave (write_pixel leaves it to us)
+                    const uint64_t dm = __ballot(done);
+                    if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
+                        atomicAdd(P.pixels_done, static_cast<uint32_t>(__popcll(dm)));
+                }
                 if (done) {
-                    write_pixel(P, x, lr, ps);
+                    ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
+                    write_pixel(P, x, lr, ps, false);
                     need = true;
                 } else if (park) {  // park at the sample boundary
+                    ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
                     Parked q;
                     q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
                     q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
@@ -1716,6 +1725,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.defocus_angle = cam->defocus_angle;
     P.W = cam->img_width;
     P.s = samples_sqrt;
+    P.s_magic = samples_sqrt >= 2 && samples_sqrt <= 1625
+                    ? static_cast<uint32_t>(((1ull << 32) + samples_sqrt - 1) / samples_sqrt)
+                    : 0u;
     P.n_off = samples_sqrt ? samples_sqrt * samples_sqrt : 1;
     P.max_depth = cam->max_depth;
     P.row_begin = sh.row_begin;
