@@ -371,6 +371,34 @@ struct PixelLoc {
     }
 };
 
+// get_ray (camera.rs:400-420) with the defocus disk point (px, py) already drawn:
+// the lattice offset of sample k, the origin, the direction; starts a fresh path.
+__device__ __forceinline__ void ray_from_disk(const KParams &P, const PixelLoc &pl, uint32_t k, double px,
+                                              double py, Path &p) {
+    double offx, offy, offz;
+    if (P.s == 0) {
+        offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
+    } else {
+        const uint32_t ly = P.s_magic ? __umulhi(k, P.s_magic) : k / P.s, lx = k - ly * P.s;
+        const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
+        offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
+        offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
+        offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
+    }
+    const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
+    if (P.defocus_angle <= 0.) {
+        p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
+    } else {
+        p.ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
+        p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
+        p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
+    }
+    p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
+    p.depth = 0;
+    p.prev = -1;
+    p.stk.clear();
+}
+
 // camera.rs:400-420 + offset_lattice (422-450) + defocus_disk_sample (452-456):
 // the ray of lattice sample k; starts a fresh path.
 __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, uint32_t k, U128 &rng,
@@ -1322,20 +1350,83 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             STAMP(0);  // 0: loop top, refill
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
             STAMP(1);  // 1: hit tail (exact candidates, cut check)
-            double cr, cg, cb;
-            const bool ended = shade(P, sph, sv.shd, best, bt, a, p, ps.rng, P.spill, gid, stride, cr, cg, cb, stp);
-            STAMP(3);  // 3: hit record + scatter / sky
+            // ---- segment end: HitRecord + scatter (materials.rs:22-111) or the sky, the
+            // sample boundary, and ONE rejection loop for every lane's draws --
+            // random_unit_vec (Lambertian / Metal, vec3.rs:218-232) and, for a lane whose
+            // sample ended, the next sample's defocus disk (vec3.rs:270-277), in that
+            // lane's own order (the scatter's draws first). The wave pays the max over
+            // lanes of their combined tries instead of two separate maxima. Decisions
+            // that need no draw (fold, done, park) come before the loop, every action
+            // that depends on the RNG state (park entry, new ray) after it.
+            const uint32_t kind = best >= 0 ? sv.shd[best].kind : 3u;  // 3: the sky
+            double vx = 0., vy = 0., vz = 0.;
+            if (kind != RTW_LAMBERTIAN) {  // unit(dir), vec3.rs:183-185
+                const double l = __builtin_sqrt(a);
+                vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+            }
+            double cr = 0., cg = 0., cb = 0.;  // leaf colour of a sample that ends here
+            bool ended = true;
+            double fz = 1.;  // Lambertian / Metal: new direction = p.d + u fz (p.d = n or the reflection)
+            if (best < 0) {  // camera.rs:395-397
+                const double t = 0.5 * (vy + 1.0);
+                const double om = 1.0 - t;
+                cr = om + 0.5 * t, cg = om + 0.7 * t, cb = om + t;
+            } else {
+                // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
+                const double4 S = sph[best];
+                const ShadeRec M = sv.shd[best];
+                const double r = M.r;
+                const double hx = p.dx * bt + p.ox, hy = p.dy * bt + p.oy, hz = p.dz * bt + p.oz;
+                double nx = (hx - S.x) / r, ny = (hy - S.y) / r, nz = (hz - S.z) / r;
+                const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
+                if (!front) nx = -nx, ny = -ny, nz = -nz;
+                ended = p.depth + 1u >= P.max_depth;  // ray_color(depth >= max) -> black
+                double ndx = nx, ndy = ny, ndz = nz;
+                if (kind == RTW_METAL) {  // materials.rs:52-63: reflect(unit(dir), n) + fuzz u
+                    const double dt = vx * nx + vy * ny + vz * nz;
+                    ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2., ndz = vz - (nz * dt) * 2.;
+                    fz = M.p;
+                } else if (kind == RTW_DIELECTRIC) {  // materials.rs:83-111 (attenuation 1)
+                    const double ratio = front ? M.a0 : M.p;  // host: a0 = 1/ir, a1 = r0*r0
+                    const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+                    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
+                    bool refl = ratio * sin_t > 1.;
+                    if (!refl) {
+                        const double r0 = M.a1;
+                        const double q = 1. - cos_t;
+                        const double schlick = r0 + (1. - r0) * (q * ((q * q) * (q * q)));
+                        refl = schlick > xs_next_01(ps.rng);
+                    }
+                    if (refl) {  // vec3.rs:252-257
+                        const double dt = vx * nx + vy * ny + vz * nz;
+                        ndx = vx - (nx * dt) * 2., ndy = vy - (ny * dt) * 2., ndz = vz - (nz * dt) * 2.;
+                    } else {  // vec3.rs:259-268 (its cos is cos_t: the same expression)
+                        const double qx = (vx + nx * cos_t) * ratio, qy = (vy + ny * cos_t) * ratio,
+                                     qz = (vz + nz * cos_t) * ratio;
+                        const double w = -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
+                        ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
+                    }
+                }
+                if (kind != RTW_DIELECTRIC) {  // the bounce's attenuation row
+                    if (ended) cr = M.a0 * 0., cg = M.a1 * 0., cb = M.a2 * 0.;  // att x black
+                    else p.stk.push(static_cast<uint32_t>(best), P.spill, stride, gid);
+                }
+                p.ox = hx, p.oy = hy, p.oz = hz;
+                p.dx = ndx, p.dy = ndy, p.dz = ndz;
+                p.prev = best;
+                ++p.depth;
+            }
+            STAMP(6);  // 6: hit record + scatter without draws
+            bool done = false, park = false;
             if (ended) {
                 fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
                 acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
-                STAMP(7);  // 7: fold + pixel sum
-                const bool done = ++ps.k >= P.n_off;
+                done = ++ps.k >= P.n_off;
                 // park: the budget is spent, the rate runs away, or -- once the
                 // cursor is dry, so drain groups are about to be plentiful -- the
                 // estimated remaining work exceeds P.tail_segs
-                const bool park =
-                    !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
-                              (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
+                park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
+                                 (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
                 if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
                     atomicAdd(P.diag + 2 * pix, pseg);
                     __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
@@ -1347,6 +1438,48 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
                         atomicAdd(P.pixels_done, static_cast<uint32_t>(__popcll(dm)));
                 }
+            }
+            STAMP(7);  // 7: fold + pixel sum + decisions
+            // the draws: phase 1 = random_unit_vec (3 per try, accept len^2 <= 1),
+            // phase 2 = the defocus disk (2 per try, accept len^2 < 1); each candidate is
+            // judged in f32 first and rebuilt exactly only near the boundary
+            const bool want_u = kind <= RTW_METAL;  // Lambertian or Metal
+            const bool want_disk = ended && !done && !park && !(P.defocus_angle <= 0.);
+            uint32_t phase = want_u ? 1u : want_disk ? 2u : 0u;
+            double ux = 0., uy = 0., uz = 0., ul2 = 1., dpx = 0., dpy = 0.;
+            while (phase) {
+                const uint32_t m0 = xs_next_m(ps.rng), m1 = xs_next_m(ps.rng);
+                uint32_t m2 = 0;
+                if (phase == 1u) m2 = xs_next_m(ps.rng);
+                const float x32 = coord32(m0), y32 = coord32(m1), z32 = phase == 1u ? coord32(m2) : 0.f;
+                const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
+                if (l32 > 1.f + kRejBand) continue;  // surely rejected
+                if (phase == 1u) {
+                    const double x = coord64(m0), y = coord64(m1), z = coord64(m2);
+                    const double l2 = x * x + y * y + z * z;
+                    if (l32 < 1.f - kRejBand || l2 <= 1.) {
+                        ux = x, uy = y, uz = z, ul2 = l2;
+                        phase = want_disk ? 2u : 0u;
+                    }
+                } else {
+                    const double px = -1. + 2. * rtw_num::next01_of(m0);
+                    const double py = -1. + 2. * rtw_num::next01_of(m1);
+                    if (l32 < 1.f - kRejBand || (px * px + py * py + 0. * 0.) < 1.) {
+                        dpx = px, dpy = py;
+                        phase = 0u;
+                    }
+                }
+            }
+            STAMP(9);  // 9: the draws
+            if (want_u && !ended) {  // materials.rs:22-37 / 52-63 with u = unit(the point)
+                const double l = __builtin_sqrt(ul2);
+                ux = ux / l, uy = uy / l, uz = uz / l;
+                double ndx = p.dx + ux * fz, ndy = p.dy + uy * fz, ndz = p.dz + uz * fz;
+                // near_zero without abs (vec3.rs:246-250): Lambertian falls back to n
+                if (kind == RTW_LAMBERTIAN && ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = p.dx, ndy = p.dy, ndz = p.dz;
+                p.dx = ndx, p.dy = ndy, p.dz = ndz;
+            }
+            if (ended) {
                 if (done) {
                     ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
                     write_pixel(P, x, lr, ps, false);
@@ -1361,7 +1494,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     ++tl.parked;
                     need = true;
                 } else {
-                    gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, ps.rng, p, stp);
+                    ray_from_disk(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, dpx, dpy, p);
                 }
             }
             STAMP(4);  // 4: fold + next sample / pixel end
