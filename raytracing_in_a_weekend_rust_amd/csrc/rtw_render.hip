@@ -790,12 +790,14 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 template <bool kLdsStack = false>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
-                                       double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr) {
+                                       double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
+                                       double *sa_out = nullptr) {
     const double4 *__restrict__ sph = sv.sph;
     const float4 *__restrict__ nodes = sv.nodes;
     const float4 *__restrict__ leaves = sv.leaves;
     int best = -1;
     const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
+    if (sa_out) *sa_out = g.sa;  // sqrt(a): the scatter's unit(dir) divides by the same value
     bool brute = !g.fast;
     if (g.fast) {
         for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
@@ -1274,10 +1276,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
 
     Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
+    double seg_sa = 0.;  // sqrt(a) of the current segment (BVH hit), reused by the scatter
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x);
+            return bvh_hit<true>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x,
+                                 &seg_sa);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -1361,7 +1365,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const uint32_t kind = best >= 0 ? sv.shd[best].kind : 3u;  // 3: the sky
             double vx = 0., vy = 0., vz = 0.;
             if (kind != RTW_LAMBERTIAN) {  // unit(dir), vec3.rs:183-185
-                const double l = __builtin_sqrt(a);
+                const double l = kMode == kBvh ? seg_sa : __builtin_sqrt(a);
                 vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
             }
             double cr = 0., cg = 0., cb = 0.;  // leaf colour of a sample that ends here
