@@ -112,8 +112,10 @@ struct Builder {
         return best_cut;
     }
 
+    // leaf id = sphere index: a candidate is its sphere (no index lookup after the walk)
     uint32_t leaf_record(uint32_t i) {
-        const uint32_t k = n_leaf++;
+        const uint32_t k = i;
+        ++n_leaf;
         float *L = &out->leaves[8 * static_cast<size_t>(k)];
         L[0] = static_cast<float>(c[3 * i]), L[1] = static_cast<float>(c[3 * i + 1]);
         L[2] = static_cast<float>(c[3 * i + 2]), L[3] = r2p[i];
@@ -217,8 +219,8 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     }
     if (out.always.size() > kMaxAlways) return false;
     const uint32_t m = static_cast<uint32_t>(rest.size());
-    out.leaves.assign(8 * static_cast<size_t>(m), 0.f);
-    out.n_leaf = m;
+    out.leaves.assign(8 * static_cast<size_t>(n), 0.f);  // indexed by sphere ("always" slots unused)
+    out.n_leaf = n;
     if (m == 0) return true;
     Builder b{centers, radii, r2p, rest, &out};
     b.median = std::getenv("RTW_BVH_MEDIAN") != nullptr;

@@ -66,8 +66,9 @@ constexpr double kHugeRatio = 16.0;     // radius > kHugeRatio x median radius -
 //   inner node id or leaf k; q6.z = slot masks: bits 0-3 occupied, bits 4-7 leaf,
 //   q7.x/.y = near-to-far child order per ray octant: byte o (octant bit k set
 //   = direction k negative) holds 4 2-bit slot indices, nearest first.
-// Leaf (32 B, two float4): {cx, cy, cz, R2'} (the pass-1 filter record) and
-// {d2, sphere index, 0, 0} with d2 >= 2 (R2' - r*r) (the filter's inflation, x2).
+// Leaf (32 B, two float4), leaf id = sphere index: {cx, cy, cz, R2'} (the pass-1
+// filter record) and {d2, sphere index, 0, 0} with d2 >= 2 (R2' - r*r) (the
+// filter's inflation, x2).
 
 RTW_HD uint32_t as_u32(float f) {
     uint32_t u;

@@ -809,7 +809,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
         }
         STAMP(5);  // 5: segment setup + always-spheres
         rtw_accel::WalkRay wr;
-        if (P.n_leaf == 0) {
+        if (P.n_node == 0) {  // every sphere is an "always" sphere
         } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
             brute = true;
         } else {
@@ -820,7 +820,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
                 if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
                     ++tl.ntest;
-                    exact_test(sph, __float_as_uint(leaves[2u * ws.cand_at(j) + 1u].y), ox, oy, oz, dx, dy, dz,
+                    exact_test(sph, ws.cand_at(j), ox, oy, oz, dx, dy, dz,
                                a, best, bt);
                 }
                 return true;

@@ -103,7 +103,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
             better(t, i, h.t, h.idx))
             h.idx = static_cast<int>(i), h.t = t;
     }
-    if (S.bvh.n_leaf == 0) return h;
+    if (S.bvh.n_node == 0) return h;
     const double mo = std::fmax(std::fmax(std::fabs(o[0]), std::fabs(o[1])), std::fabs(o[2]));
     const double sa = std::sqrt(a);
     WalkRay wr;
@@ -131,7 +131,7 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
     }
     for (uint32_t j = 0; j < nc; ++j) {
         const uint32_t leaf = ws.cand_at(j);
-        const uint32_t i = as_u32(S.bvh.leaves[8 * leaf + 5]);
+        const uint32_t i = leaf;  // leaf id = sphere index
         double t;
         if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
                            S.c[3 * i + 2], S.rr[i], t) &&
