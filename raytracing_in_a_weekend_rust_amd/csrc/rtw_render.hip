@@ -53,6 +53,7 @@ constexpr int kCounters = 10;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
 constexpr uint32_t kTailSegs = 768;     // dry-cursor parking: estimated segments left (RTW_TAIL)
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
+constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 
 // Scene::hit strategies (one kernel instantiation each)
@@ -112,7 +113,9 @@ struct KParams {
     uint32_t n_node, n_leaf, n_always, seg_budget;
     uint32_t order, heavy_per_block;
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
-    uint32_t tail_segs, _pad5;  // once the cursor is dry: park pixels with more estimated work left
+    uint32_t tail_segs;         // once the cursor is dry: park pixels with more estimated work left
+    uint32_t join_at;           // priority waves join the cursor once it has handed out this many
+                                // pixels and the park queue is idle (0xffffffff: never)
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
     uint32_t n_nbr;             // inside-cut list entries
     uint32_t s_magic;           // ceil(2^32 / s) for k / s by a multiply-high (s <= 1625), else 0
@@ -1290,9 +1293,60 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     if (P.diag && blockIdx.x == 0 && threadIdx.x == 0)  // diagnostic: launch start after the pixels
         P.diag[2 * npix] = static_cast<uint32_t>(t_start);
+    // priority waves: drain parked pixels from the start; with P.join_at they leave
+    // for the cursor once it has handed out join_at pixels and no published entry is
+    // unclaimed (claims by compare-and-swap, so a leaving wave holds no ticket that
+    // may never be published), and then count as cursor waves
+    bool cursor_wave = !heavy_wave;
     if (heavy_wave) {
         __builtin_amdgcn_s_setprio(3);
-    } else {
+        const uint32_t sub = threadIdx.x & (kCoopG - 1u);
+        const int gl = static_cast<int>(lane & ~(kCoopG - 1u));
+        uint32_t cseg = 0;
+        while (P.join_at != 0xffffffffu) {
+            uint32_t t = 0, state = 0;  // 1: ticket t, 2: join the cursor
+            if (sub == 0) {
+                for (uint32_t spins = 0;; ++spins) {
+                    const uint32_t c = ld_rlx(P.park_cursor), n = ld_rlx(P.park_count);
+                    if (c < n) {
+                        if (atomicCAS(P.park_cursor, c, c + 1u) == c) {
+                            t = c;
+                            while (ld_rlx(P.park_flag + t) != 1u) __builtin_amdgcn_s_sleep(2);
+                            state = 1;
+                            break;
+                        }
+                        continue;
+                    }
+                    if (ld_rlx(P.pix_cursor) >= P.join_at) {
+                        state = 2;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(16);
+                    if ((spins & 1023u) == 1023u &&
+                        __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
+                        atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
+                        state = 2;
+                        break;
+                    }
+                }
+            }
+            t = __shfl(t, gl);
+            state = __shfl(state, gl);
+            if (state == 2) {
+                cursor_wave = true;
+                __builtin_amdgcn_s_setprio(0);
+                break;
+            }
+            Parked q;
+            unsigned long long *w = reinterpret_cast<unsigned long long *>(&q);
+            gu64 *src = (gu64 *)(P.park + t);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+        }
+        tl.seg += cseg;
+    }
+    if (cursor_wave) {
         bool need = true;  // lane holds no pixel
         bool dry = false;  // wave-uniform: the cursor ran dry
         uint32_t x = 0, lr = 0, pseg = 0;
@@ -2067,7 +2121,21 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
-        P.n_cursor_waves = grid_p * (wpb - heavy);
+        // priority waves join the cursor once it has handed out kJoinPct % of the
+        // pixels (RTW_JOIN=percent, 0 = never): the hot pixels (handed out first) have
+        // parked and been drained by then, and the waves would idle (measured: 25-50 %
+        // all 159-161 ms, never 168-171 ms, 10 % 173 ms)
+        // Only shards of >= 4 x the cursor lanes: in smaller ones the first fill already
+        // hands out most pixels, and parks keep coming while the waves would be gone
+        // (N=2 rank: 93 -> 111 ms, N=4: 79 -> 103 ms with the join).
+        const uint64_t cursor_lanes = static_cast<uint64_t>(grid_p) * (wpb - heavy) * 64u;
+        double join_pct = npix >= 4u * cursor_lanes ? kJoinPct : 0.;
+        if (const char *e = std::getenv("RTW_JOIN")) join_pct = std::atof(e);
+        P.join_at = join_pct > 0. ? static_cast<uint32_t>(std::min(npix, static_cast<uint64_t>(
+                                        join_pct / 100. * static_cast<double>(npix))))
+                                  : 0xffffffffu;
+        // waves that signal the end of their cursor loop: priority waves too when they join
+        P.n_cursor_waves = P.join_at != 0xffffffffu ? grid_p * wpb : grid_p * (wpb - heavy);
         P.rate_k = 16, P.rate_x = 16;
         P.tail_segs = small_shard ? 0xffffffffu : kTailSegs;
         if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));

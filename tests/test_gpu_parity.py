@@ -176,6 +176,7 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0", "rate1"),                        # rate-based parking of nearly every pixel
     ("2", "0", "order0"), ("2", "0", "order1"),  # row-major / bottom-up hand-out (default: by cost)
     ("2", "0.3", "coopg16"), ("1", "0.3", "coopg16"),  # 16-lane drain groups (default: one wave)
+    ("2", "0.3", "join5"), ("2", "1.5", "join50"),  # priority waves join the cursor (RTW_JOIN %)
 ]
 
 
@@ -192,6 +193,7 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_RATE_K", "2" if coop == "rate1" else "16")
     monkeypatch.setenv("RTW_ORDER", {"order0": "0", "order1": "1"}.get(coop, "2"))
     monkeypatch.setenv("RTW_COOPG", "16" if coop == "coopg16" else "64")
+    monkeypatch.setenv("RTW_JOIN", {"join5": "5", "join50": "50"}.get(coop, "0"))
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
     fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
     ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
