@@ -968,14 +968,23 @@ __global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
 
 // Per-pixel RNG children (copy_reset, camera.rs:269-272) of the shard's pixels, in
 // shard order, by device jump-ahead: the persistent kernel refills lanes from it.
+// One thread per run of kSeedRun pixels of a row: one jump-ahead to the run's
+// first pixel, then the serial chain's own step per pixel (T^(p+1) = T(T^p)).
+constexpr uint32_t kSeedRun = 8;
 __global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
-    if (i >= npix) return;
-    const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
+    const uint32_t runs = (P.W + kSeedRun - 1) / kSeedRun;
+    const uint64_t t = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    if (t >= static_cast<uint64_t>(P.n_rows) * runs) return;
+    const uint32_t lr = static_cast<uint32_t>(t / runs);
+    const uint32_t x0 = static_cast<uint32_t>(t - static_cast<uint64_t>(lr) * runs) * kSeedRun;
     const uint32_t y = P.row_begin + lr * P.row_step;
-    P.seeds[i] = child_of(jump_state(U128{P.seed_lo, P.seed_hi}, static_cast<uint64_t>(y) * P.W + x,
-                                     P.jump, P.jump_bits));
+    U128 s = jump_state(U128{P.seed_lo, P.seed_hi}, static_cast<uint64_t>(y) * P.W + x0, P.jump, P.jump_bits);
+    U128 *out = P.seeds + static_cast<uint64_t>(lr) * P.W + x0;
+    const uint32_t n = min(kSeedRun, P.W - x0);
+    for (uint32_t k = 0; k < n; ++k) {
+        out[k] = child_of(s);
+        xs_step(s);
+    }
 }
 
 // Shared words of the park queue (agent scope): relaxed atomics; payload stored
@@ -2060,7 +2069,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
         // per-pixel seeds (a separate launch: measured 0.7 ms faster than deriving
         // them inside the LDS-heavy cost probe)
-        hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((npix + kBlock - 1) / kBlock)),
+        const uint64_t seed_threads = static_cast<uint64_t>(P.n_rows) * ((P.W + kSeedRun - 1) / kSeedRun);
+        hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((seed_threads + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
         // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
