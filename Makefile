@@ -15,9 +15,14 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra 
 
 all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check
 
-$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+$(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# f32 fast mode: FMA contraction allowed (its own file, its own flags)
+$(OUT)/rtw_fast.o: $(SRC)/rtw_fast.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h include/rtw_capi.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(filter-out -ffp-contract=off,$(HIPFLAGS)) -ffp-contract=fast -c $< -o $@
 
 $(OUT)/rtw_accel_build.o: $(SRC)/host/rtw_accel_build.cpp $(SRC)/rtw_accel.h
 	@mkdir -p $(OUT)
@@ -36,7 +41,7 @@ $(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_h
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
+$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
 
 $(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
@@ -49,7 +54,7 @@ oracle:
 stamps: $(OUT)/librtw_stamps.so
 $(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
 	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
-$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
+$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
 asm: $(SRC)/rtw_render.hip

@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                    help="N>1: weak = one whole frame per rank (seed SEED+rank), no collective; "
                         "strong = the one frame row-cyclically sharded + RCCL all_gather")
+    p.add_argument("--mode", choices=("parity", "fast"), default="parity",
+                   help="parity = f64 bit-exact (the headline); fast = the f32 mode with "
+                        "independent per-sample streams (statistical parity, tests/test_gpu_fast.py)")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU leg")
     p.add_argument("--cpu-row-stride", type=int, default=0,
                    help="oracle renders every k-th row (0 = auto, ~10-30 s)")
@@ -120,10 +123,13 @@ def main():
     sess = rtw.Session(local)
     sess.set_scene(sph, ns, mt, nm)
     dev = torch.device("cuda", local)
-    fb = torch.zeros((rm, W, 3), dtype=torch.float64, device=dev)  # padded tile
+    fast = a.mode == "fast"
+    fdt = torch.float32 if fast else torch.float64
+    fb = torch.zeros((rm, W, 3), dtype=fdt, device=dev)  # padded tile
+    render = sess.render_fast if fast else sess.render
     if world > 1 and not weak:
-        gathered = torch.empty((world * rm, W, 3), dtype=torch.float64, device=dev)
-        image = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        gathered = torch.empty((world * rm, W, 3), dtype=fdt, device=dev)
+        image = torch.empty((H, W, 3), dtype=fdt, device=dev)
         index = shard.unpermute_index(world, H, dev)
     stream = torch.cuda.current_stream(dev)
     kernel_ms = []
@@ -132,8 +138,8 @@ def main():
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
-        sess.render(cam.raw, s, render_seed, fb.data_ptr(), stream=stream.cuda_stream,
-                    shard=(rb, rstep, rows_local))
+        render(cam.raw, s, render_seed, fb.data_ptr(), stream=stream.cuda_stream,
+               shard=(rb, rstep, rows_local))
         ev1.record(stream)
         if world > 1 and not weak:  # RCCL all_gather of the row tiles + un-permute
             shard.gather_image(fb, world, H, gathered, image, index)
@@ -172,9 +178,10 @@ def main():
     else:
         exec_flop = brute_flop
     achieved = brute_flop / (kms / 1e3) / 1e12
+    peak = FP32_VECTOR_PEAK if fast else FP64_VECTOR_PEAK
     executed = exec_flop / (kms / 1e3) / 1e12
     valu = None  # VALU issue utilisation from the committed PMC pass (profiles/pmc_insts.json)
-    if os.path.exists(INSTS_FILE) and world == 1:
+    if os.path.exists(INSTS_FILE) and world == 1 and not fast:
         try:
             with open(INSTS_FILE) as f:
                 pi = json.load(f)
@@ -202,7 +209,7 @@ def main():
         try:
             with open(PMC_FILE) as f:
                 pm = json.load(f)
-            if pm.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}" and world == 1:
+            if pm.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}" and world == 1 and not fast:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -220,7 +227,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32" if fast else "f64",
             "data": "synthetic (the reference's own procedural final scene, fixed seed)",
             "config": {"workload": f"complex_{W}x{H}_s{s}_d{DEPTH}", "width": W, "height": H,
                        "samples_sqrt": s, "spp": n_off, "max_depth": DEPTH,
@@ -228,16 +235,20 @@ def main():
                        "parallelism": (f"frame-per-rank x{world} (render seed SEED+rank), no collective"
                                        if weak else f"row-cyclic x{world}" +
                                        (" + rccl all_gather" if world > 1 else "")),
-                       "mode": "parity_f64 (bit-exact)"},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": FP64_VECTOR_PEAK,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP64_VECTOR_PEAK, 4),
-                         "traffic": traffic, "kernel": "rtw_render_persist (+ 7 small launches)",
+                       "mode": ("fast_f32 (statistical parity; xoroshiro64** per (pixel, sample))"
+                                if fast else "parity_f64 (bit-exact)")},
+            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "traffic": traffic,
+                         "kernel": "rtw_fast_render" if fast else "rtw_render_persist (+ 7 small launches)",
                          "kernel_ms": round(kms, 3),
                          "algorithmic_flop_per_launch": brute_flop,
                          "executed_flop_per_launch": exec_flop,
                          "executed_tflops": round(executed, 3),
                          "executed_frac_of_fp32_peak": round(executed / FP32_VECTOR_PEAK, 4),
-                         "note": "achieved = SURVEY 8(d)'s algorithmic work (segments x n_spheres x 17 "
+                         "note": ("fast mode: achieved = the same algorithmic brute-force work (segments x "
+                                  "n_spheres x 17 FLOP) in f32 / kernel time, against the FP32 vector peak"
+                                  if fast else None) or "achieved = SURVEY 8(d)'s algorithmic work (segments x n_spheres x 17 "
                                  "FLOP, the reference's f64 brute-force Scene::hit) / HIP-event kernel "
                                  "time, against the FP64 vector peak (parity mode is f64). The exact BVH "
                                  "and f32 filter reach that rate without executing it "
@@ -251,7 +262,8 @@ def main():
                       "brute_segments": st.brute_segments, "lds_bytes": st.lds_bytes,
                       "parked_pixels": st.parked_pixels,
                       "segments": st.segments, "segments_per_sample": round(st.segments / max(1, st.samples), 4),
-                      "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
+                      "lane_utilization": (round(st.segments / max(1, 64 * st.wave_iterations), 4)
+                                           if not fast else None),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
                       "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),

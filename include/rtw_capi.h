@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 3
+#define RTW_ABI_VERSION 4
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -158,6 +158,12 @@ int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32
                         rtw_u128 seed, const rtw_shard *shard, double *out_rgb,
                         rtw_stats *stats);
 
+/* rtw_threaded_render in f32 fast mode (see rtw_session_render_fast). */
+int rtw_threaded_render_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                             const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                             rtw_u128 seed, const rtw_shard *shard, float *out_rgb,
+                             rtw_stats *stats);
+
 /* Device-resident sessions: scene uploaded once, renders enqueued on a caller
  * stream into a caller device buffer (inputs already in HBM when timing). */
 typedef struct rtw_session rtw_session;
@@ -171,6 +177,16 @@ int rtw_session_set_scene(rtw_session *s, const rtw_sphere *spheres, uint32_t n_
 int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
                        rtw_u128 seed, const rtw_shard *shard, double *out_rgb_device,
                        void *hip_stream);
+/* f32 fast mode (SURVEY 8(c) "Fast mode"; the ABI sketch's rtw_mode FAST_F32):
+ * the same camera, scene, materials and depth rule in f32, with independent
+ * xoroshiro64** streams per (pixel, lattice sample) instead of the reference's
+ * per-pixel XorShift chain. NOT bit-exact: statistically equal to the parity
+ * render (tests/test_gpu_fast.py). Deterministic, and any shard reproduces the
+ * unsharded pixels bit-for-bit. Output: n_rows*W*3 f32. Per-sample colours are
+ * clamped to [0, min(65536, 2^31 / spp)] (NaN -> 0). */
+int rtw_session_render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
+                            rtw_u128 seed, const rtw_shard *shard, float *out_rgb_device,
+                            void *hip_stream);
 /* Waits for the session's last render and reports its statistics. */
 int rtw_session_stats(rtw_session *s, rtw_stats *out);
 /* Diagnostic (not part of the reference surface): per-pixel records of the last

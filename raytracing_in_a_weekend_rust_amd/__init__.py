@@ -5,6 +5,6 @@ include/rtw_capi.h. See DESIGN.md."""
 from ._capi import LIB_PATH, RtwError  # noqa: F401  (raises ImportError if librtw.so is missing)
 from .api import (DEFAULT_SEED, Camera, Dielectric, Lambertian, Metal, Scene,  # noqa: F401
                   SceneBuilder, Session, Sphere, builtin_scene, device_count, format_ppm,
-                  render_flat, seed_children, write_ppm, xorshift_next_01, xorshift_next_int)
+                  render_flat, render_flat_fast, seed_children, write_ppm, xorshift_next_01, xorshift_next_int)
 
 __version__ = "0.1.0"

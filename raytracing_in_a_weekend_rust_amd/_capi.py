@@ -107,12 +107,17 @@ SIGNATURES = {
     "rtw_threaded_render": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                       C.c_uint32, C.c_uint32, U128, _P(Shard),
                                       _P(C.c_double), _P(Stats)]),
+    "rtw_threaded_render_fast": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
+                                           C.c_uint32, C.c_uint32, U128, _P(Shard),
+                                           _P(C.c_float), _P(Stats)]),
     "rtw_session_create": (C.c_int, [C.c_int, _P(C.c_void_p)]),
     "rtw_session_destroy": (C.c_int, [C.c_void_p]),
     "rtw_session_set_scene": (C.c_int, [C.c_void_p, _P(Sphere), C.c_uint32, _P(Material),
                                         C.c_uint32]),
     "rtw_session_render": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, _P(Shard),
                                      C.c_void_p, C.c_void_p]),
+    "rtw_session_render_fast": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, _P(Shard),
+                                          C.c_void_p, C.c_void_p]),
     "rtw_session_stats": (C.c_int, [C.c_void_p, _P(Stats)]),
     "rtw_session_diag": (C.c_int, [C.c_void_p, _P(C.c_uint32), C.c_uint64]),
     "rtw_probe_device_seeds": (C.c_int, [C.c_int, U128, C.c_uint64, C.c_uint64, _P(U128)]),

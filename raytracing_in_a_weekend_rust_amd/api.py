@@ -197,6 +197,20 @@ def render_flat(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, seed=D
     return fb, st
 
 
+def render_flat_fast(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, seed=DEFAULT_SEED,
+                     shard=None):
+    """rtw_threaded_render_fast (f32 fast mode, statistical parity): host buffers in,
+    (n_rows x W x 3 f32, Stats) out."""
+    sh = _shard(shard)
+    n_rows = cam.img_height if sh is None else sh.n_rows
+    fb = np.zeros((n_rows, cam.img_width, 3), dtype=np.float32)
+    st = capi.Stats()
+    check(lib.rtw_threaded_render_fast(C.byref(cam), sph, n_sph, mats, n_mats, samples_sqrt,
+                                       capi.U128.of(seed), C.byref(sh) if sh is not None else None,
+                                       fb.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
+    return fb, st
+
+
 def format_ppm(fb: np.ndarray) -> bytes:
     fb = np.ascontiguousarray(fb, dtype=np.float64)
     h, w = fb.shape[0], fb.shape[1]
@@ -254,6 +268,14 @@ class Session:
         check(lib.rtw_session_render(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
                                      C.byref(sh) if sh is not None else None,
                                      C.c_void_p(out_dev_ptr), C.c_void_p(stream or 0)))
+
+    def render_fast(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int,
+                    stream: int | None = None, shard=None):
+        """f32 fast mode into an n_rows x W x 3 f32 device buffer."""
+        sh = _shard(shard)
+        check(lib.rtw_session_render_fast(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
+                                          C.byref(sh) if sh is not None else None,
+                                          C.c_void_p(out_dev_ptr), C.c_void_p(stream or 0)))
 
     def stats(self) -> capi.Stats:
         st = capi.Stats()

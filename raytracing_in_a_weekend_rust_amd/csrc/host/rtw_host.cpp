@@ -364,7 +364,7 @@ using namespace rtw;
 
 extern "C" {
 
-const char *rtw_version(void) { return "rtw-mi355x 0.3.0 (abi 3, gfx950)"; }
+const char *rtw_version(void) { return "rtw-mi355x 0.4.0 (abi 4, gfx950)"; }
 const char *rtw_last_error(void) { return rtw::last_error(); }
 
 int rtw_camera_new(uint32_t img_height, uint32_t img_width, uint32_t max_depth,

@@ -33,6 +33,7 @@
 
 #include "rtw_accel.h"
 #include "rtw_capi.h"
+#include "rtw_fast.h"
 #include "rtw_numeric.h"
 #include "host/rtw_host.h"
 #include "host/rtw_internal.h"
@@ -1721,6 +1722,12 @@ struct rtw_session {
     uint32_t *d_always = nullptr;
     uint32_t n_node = 0, n_leaf = 0, n_always = 0;
     bool has_bvh = false;
+    uint32_t bvh_depth = 0;
+    // f32 fast mode (rtw_fast.h): per-sphere geometry / material rows / kinds
+    float4 *d_fgeo = nullptr, *d_fmat = nullptr;
+    uint32_t *d_fkind = nullptr, *d_fcursor = nullptr;
+    unsigned long long *d_fcount = nullptr;
+    bool last_fast = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipStream_t last_stream = nullptr;
     bool pending = false;
@@ -1764,11 +1771,13 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
     dev_free(s->d_sph), dev_free(s->d_filt);
     dev_free(s->d_shade), dev_free(s->d_nbr), dev_free(s->d_trap);
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
+    dev_free(s->d_fgeo), dev_free(s->d_fmat), dev_free(s->d_fkind);
+    s->d_fgeo = s->d_fmat = nullptr, s->d_fkind = nullptr;
     s->d_sph = nullptr, s->d_filt = nullptr;
     s->d_shade = nullptr, s->d_nbr = nullptr, s->n_nbr = 0, s->d_trap = nullptr;
     s->d_nodes = nullptr, s->d_leaves = nullptr, s->d_always = nullptr;
     s->has_bvh = false, s->scene_set = false;
-    s->n_node = s->n_leaf = s->n_always = 0;
+    s->n_node = s->n_leaf = s->n_always = s->bvh_depth = 0;
     const uint32_t npad = (n + kChunk - 1) / kChunk * kChunk;
     std::vector<double4> a(n ? n : 1);
     // padding records can never be candidates (R2' = -inf -> disc = -inf)
@@ -1865,8 +1874,35 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
                                    hipMemcpyHostToDevice));
             s->n_node = bvh.n_node, s->n_leaf = bvh.n_leaf;
             s->n_always = static_cast<uint32_t>(bvh.always.size());
+            s->bvh_depth = bvh.depth;
             s->has_bvh = true;
         }
+    }
+    // fast-mode rows: f32 geometry, material row, kind
+    {
+        std::vector<float4> fg(n ? n : 1), fm(n ? n : 1);
+        std::vector<uint32_t> fk(n ? n : 1, 0);
+        for (uint32_t i = 0; i < n; ++i) {
+            const rtw_material &M = m[sp[i].mat];
+            fg[i] = make_float4(static_cast<float>(sp[i].center[0]), static_cast<float>(sp[i].center[1]),
+                                static_cast<float>(sp[i].center[2]), static_cast<float>(sp[i].radius));
+            if (M.kind == RTW_DIELECTRIC) {
+                const double r0 = (1. - M.ir) / (1. + M.ir);
+                fm[i] = make_float4(static_cast<float>(1. / M.ir), static_cast<float>(M.ir),
+                                    static_cast<float>(r0 * r0), 0.f);
+            } else {
+                fm[i] = make_float4(static_cast<float>(M.albedo[0]), static_cast<float>(M.albedo[1]),
+                                    static_cast<float>(M.albedo[2]),
+                                    M.kind == RTW_METAL ? static_cast<float>(M.fuzz) : 0.f);
+            }
+            fk[i] = M.kind;
+        }
+        HIPCHECK(hipMalloc(&s->d_fgeo, fg.size() * sizeof(float4)));
+        HIPCHECK(hipMalloc(&s->d_fmat, fm.size() * sizeof(float4)));
+        HIPCHECK(hipMalloc(&s->d_fkind, fk.size() * sizeof(uint32_t)));
+        HIPCHECK(hipMemcpy(s->d_fgeo, fg.data(), fg.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(s->d_fmat, fm.data(), fm.size() * sizeof(float4), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(s->d_fkind, fk.data(), fk.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     s->n_sph = n;
     s->n_mats = nm;
@@ -2195,12 +2231,99 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     s->last.block_threads = kBlock;
     s->last.accel = static_cast<uint32_t>(mode);
     s->last.lds_bytes = static_cast<uint32_t>(lds);
+    s->last_fast = false;
+}
+
+// f32 fast mode (rtw_fast.hip): same camera, shard and validation as render().
+void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                 const rtw_shard *shard_in, float *out, hipStream_t stream) {
+    if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
+    if (!s->scene_set) throw rtw::Error(RTW_E_ARG, "session has no scene");
+    if (cam->img_height == 0 || cam->img_width == 0)
+        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");  // camera.rs:267
+    if (samples_sqrt > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "samples_sqrt > 65535");
+    if (static_cast<uint64_t>(cam->img_height) * cam->img_width >= (1ull << 32))
+        throw rtw::Error(RTW_E_UNSUPPORTED, "fast mode: image >= 2^32 pixels");
+    const rtw_shard sh = resolve_shard(cam, shard_in);
+    rtw_fast::FastParams F{};
+    auto cp = [](float *d, const rtw_vec3 &v) {
+        d[0] = static_cast<float>(v.x), d[1] = static_cast<float>(v.y), d[2] = static_cast<float>(v.z);
+    };
+    cp(F.p00, cam->pixel00);
+    cp(F.du, cam->pixel_delta_u);
+    cp(F.dv, cam->pixel_delta_v);
+    cp(F.from, cam->look_from);
+    cp(F.ddu, cam->defocus_disk_u);
+    cp(F.ddv, cam->defocus_disk_v);
+    // offset_lattice(&pixel_delta_v, &pixel_delta_u, s) (camera.rs:243-244), in f64 then rounded
+    const rtw::Vec3 dxv = rtw::Vec3::of(cam->pixel_delta_v), dyv = rtw::Vec3::of(cam->pixel_delta_u);
+    if (samples_sqrt == 0) {
+        cp(F.pos0, (dxv / 2. + dyv / 2.).c());
+    } else {
+        const double n = static_cast<double>(samples_sqrt);
+        const rtw::Vec3 dx = dxv / n, dy = dyv / n;
+        cp(F.ldx, dx.c());
+        cp(F.ldy, dy.c());
+        cp(F.pos0, (dx / 2. + dy / 2.).c());
+    }
+    F.defocus = cam->defocus_angle > 0. ? 1u : 0u;
+    F.W = cam->img_width;
+    F.s = samples_sqrt;
+    F.n_off = samples_sqrt ? samples_sqrt * samples_sqrt : 1;
+    F.max_depth = cam->max_depth;
+    F.row_begin = sh.row_begin, F.row_step = sh.row_step, F.n_rows = sh.n_rows;
+    F.n_sph = s->n_sph;
+    // the walk's per-lane stack bounds the BVH depth it can take; deeper trees scan
+    const bool walk = s->has_bvh && rtw_fast::stack_slots(s->bvh_depth) <= rtw_fast::kMaxStack;
+    F.n_node = walk ? s->n_node : 0;
+    F.n_always = walk ? s->n_always : 0;
+    F.nodes = s->d_nodes;
+    F.always = s->d_always;
+    F.n_stack = walk ? rtw_fast::stack_slots(s->bvh_depth) : 0;
+    F.cmax = static_cast<float>(std::min(65536., 2147483648. / static_cast<double>(F.n_off)));
+    F.seed_mix = seed.lo ^ (seed.hi * 0x9e3779b97f4a7c15ull);
+    F.geo = s->d_fgeo, F.mat = s->d_fmat, F.kind = s->d_fkind;
+    F.out = out;
+    F.cursor = s->d_fcursor;
+    F.counters = s->d_fcount;
+    hipStream_t st = stream;
+    HIPCHECK(hipSetDevice(s->device));
+    HIPCHECK(hipEventRecord(s->ev0, st));
+    HIPCHECK(rtw_fast::launch(F, s->n_cu, st));
+    HIPCHECK(hipEventRecord(s->ev1, st));
+    s->last_stream = st;
+    s->pending = true;
+    s->last = rtw_stats{};
+    s->last.pixels = static_cast<uint64_t>(F.n_rows) * F.W;
+    s->last.samples = s->last.pixels * F.n_off;
+    s->last.grid_blocks = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(s->n_cu > 0 ? s->n_cu : 256) * 2,
+                                                                   (s->last.pixels + 7) / 8));
+    s->last.block_threads = rtw_fast::kBlock;
+    s->last.accel = F.n_node ? 2u : 0u;
+    bool in_lds = false;
+    s->last.lds_bytes = static_cast<uint32_t>(rtw_fast::lds_bytes(F.n_sph, F.n_node, F.n_stack, &in_lds));
+    s->last_fast = true;
 }
 
 void collect(rtw_session *s) {
     if (!s->pending) return;
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
+    if (s->last_fast) {
+        unsigned long long c[3] = {};
+        HIPCHECK(hipMemcpy(c, s->d_fcount, sizeof c, hipMemcpyDeviceToHost));
+        float ms = 0.f;
+        HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        s->last.segments = c[0];
+        s->last.node_visits = c[1];
+        s->last.sphere_tests = c[0] * s->n_sph;
+        s->last.kernel_ms = ms;
+        s->pending = false;
+        if (c[2] != s->last.pixels)  // never a silently incomplete image
+            throw rtw::Error(RTW_E_HIP, "fast render incomplete: " + std::to_string(c[2]) + " of " +
+                                            std::to_string(s->last.pixels) + " pixels written");
+        return;
+    }
     unsigned long long c[kCounters] = {};
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
     float ms = 0.f;
@@ -2244,6 +2367,8 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_cost_hist, kCostBuckets * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_fcursor, sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_fcount, 4 * sizeof(unsigned long long)));
         HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         upload_jump(s);
     } catch (...) {
@@ -2266,6 +2391,47 @@ void create_session(int device, rtw_session **out) {
         rtw::set_error(e.what());             \
         return RTW_E_ARG;                     \
     }
+
+// Host-buffer render on a cached session of $RTW_DEVICE (the blocking
+// Camera::threaded_render shape): upload, enqueue `run`, wait, download.
+template <typename T, typename Run>
+int threaded(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres, const rtw_material *mats,
+             uint32_t n_mats, const rtw_shard *shard, T *out_rgb, rtw_stats *stats, Run run) {
+    if (!cam || !out_rgb) return rtw::set_error("null argument"), RTW_E_ARG;
+    static std::mutex mu;
+    static rtw_session *cached = nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    T *d_out = nullptr;
+    RTW_GUARD_BEGIN
+    if (cam->img_height == 0 || cam->img_width == 0)
+        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
+    validate_scene(spheres, n_spheres, mats, n_mats);
+    const rtw_shard sh = resolve_shard(cam, shard);
+    const int dev = default_device();
+    if (cached && cached->device != dev) rtw_session_destroy(cached), cached = nullptr;
+    if (!cached) create_session(dev, &cached);
+    set_scene(cached, spheres, n_spheres, mats, n_mats);
+    const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(T);
+    HIPCHECK(hipMalloc(&d_out, bytes ? bytes : 8));
+    run(cached, &sh, d_out, cached->own);
+    collect(cached);
+    if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
+    HIPCHECK(hipFree(d_out));
+    d_out = nullptr;
+    if (stats) *stats = cached->last;
+    return RTW_OK;
+    }
+    catch (const rtw::Error &e) {
+        if (d_out) (void)hipFree(d_out);
+        rtw::set_error(e.what());
+        return e.code;
+    }
+    catch (const std::exception &e) {
+        if (d_out) (void)hipFree(d_out);
+        rtw::set_error(e.what());
+        return RTW_E_ARG;
+    }
+}
 
 extern "C" {
 
@@ -2296,6 +2462,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
     dev_free(s->d_pcost);
+    dev_free(s->d_fgeo), dev_free(s->d_fmat), dev_free(s->d_fkind), dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
@@ -2318,6 +2485,16 @@ int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_s
     if (!s) return rtw::set_error("null session"), RTW_E_ARG;
     RTW_GUARD_BEGIN
     render(s, cam, samples_sqrt, seed, shard, out_rgb_device, static_cast<hipStream_t>(hip_stream));
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+int rtw_session_render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
+                            rtw_u128 seed, const rtw_shard *shard, float *out_rgb_device,
+                            void *hip_stream) {
+    if (!s) return rtw::set_error("null session"), RTW_E_ARG;
+    RTW_GUARD_BEGIN
+    render_fast(s, cam, samples_sqrt, seed, shard, out_rgb_device, static_cast<hipStream_t>(hip_stream));
     return RTW_OK;
     RTW_GUARD_END
 }
@@ -2345,40 +2522,19 @@ int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap) {
 int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
                         const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
                         rtw_u128 seed, const rtw_shard *shard, double *out_rgb, rtw_stats *stats) {
-    if (!cam || !out_rgb) return rtw::set_error("null argument"), RTW_E_ARG;
-    static std::mutex mu;
-    static rtw_session *cached = nullptr;
-    std::lock_guard<std::mutex> lock(mu);
-    double *d_out = nullptr;
-    RTW_GUARD_BEGIN
-    if (cam->img_height == 0 || cam->img_width == 0)
-        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
-    validate_scene(spheres, n_spheres, mats, n_mats);
-    const rtw_shard sh = resolve_shard(cam, shard);
-    const int dev = default_device();
-    if (cached && cached->device != dev) rtw_session_destroy(cached), cached = nullptr;
-    if (!cached) create_session(dev, &cached);
-    set_scene(cached, spheres, n_spheres, mats, n_mats);
-    const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(double);
-    HIPCHECK(hipMalloc(&d_out, bytes ? bytes : 8));
-    render(cached, cam, samples_sqrt, seed, &sh, d_out, cached->own);
-    collect(cached);
-    if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
-    HIPCHECK(hipFree(d_out));
-    d_out = nullptr;
-    if (stats) *stats = cached->last;
-    return RTW_OK;
-    }
-    catch (const rtw::Error &e) {
-        if (d_out) (void)hipFree(d_out);
-        rtw::set_error(e.what());
-        return e.code;
-    }
-    catch (const std::exception &e) {
-        if (d_out) (void)hipFree(d_out);
-        rtw::set_error(e.what());
-        return RTW_E_ARG;
-    }
+    return threaded(cam, spheres, n_spheres, mats, n_mats, shard, out_rgb, stats,
+                    [&](rtw_session *s, const rtw_shard *sh, double *d, hipStream_t st) {
+                        render(s, cam, samples_sqrt, seed, sh, d, st);
+                    });
+}
+
+int rtw_threaded_render_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                             const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                             rtw_u128 seed, const rtw_shard *shard, float *out_rgb, rtw_stats *stats) {
+    return threaded(cam, spheres, n_spheres, mats, n_mats, shard, out_rgb, stats,
+                    [&](rtw_session *s, const rtw_shard *sh, float *d, hipStream_t st) {
+                        render_fast(s, cam, samples_sqrt, seed, sh, d, st);
+                    });
 }
 
 int rtw_probe_device_seeds(int device, rtw_u128 seed, uint64_t first_pixel, uint64_t count,
