@@ -4,13 +4,15 @@
 //
 // Extra flags (the reference hard-codes or time-seeds these): --depth (MAX_DEPTH,
 // mod.rs:43), --seed (both XorShift::default seeds, mod.rs:67 / camera.rs:255),
-// --scene (the other builders of mod.rs), --out. --preview is accepted and
+// --scene (the other builders of mod.rs), --out, --mode parity|fast (fast: the
+// f32 statistical mode, rtw_threaded_render_fast). --preview is accepted and
 // ignored: the winit preview window (application/mod.rs) is out of scope.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "rtw_host.h"
 
@@ -22,6 +24,7 @@ struct Config {  // main.rs:13-29
     std::string scene = "complex", out = "img.ppm";
     unsigned long long seed = 0;
     bool seed_set = false;
+    bool fast = false;
 };
 
 bool parse_u32(const char *s, uint32_t &v) {
@@ -52,6 +55,13 @@ Config parse_args(int argc, char **argv) {
         else if (a == "--seed" && next) c.seed = std::strtoull(next, nullptr, 0), c.seed_set = true;
         else if (a == "--scene" && next) c.scene = next;
         else if (a == "--out" && next) c.out = next;
+        else if (a == "--mode" && next) {
+            if (std::strcmp(next, "fast") && std::strcmp(next, "parity")) {
+                std::fprintf(stderr, "Usage: --mode parity|fast\n");
+                std::exit(1);
+            }
+            c.fast = !std::strcmp(next, "fast");
+        }
         else if (a == "--help") {
             std::printf("Use the application like this:\n");
             std::printf("\t-h --height\t:\tSet the height of the image\n");
@@ -62,6 +72,7 @@ Config parse_args(int argc, char **argv) {
             std::printf("\t--seed N\t:\tXorShift seed for scene and render (reference: wall-clock ms)\n");
             std::printf("\t--scene NAME\t:\tcomplex | simple | threads | super_simple | three_lambertian\n");
             std::printf("\t--out PATH\t:\tOutput PPM (reference: img.ppm)\n");
+            std::printf("\t--mode M\t:\tparity (f64, bit-exact; default) | fast (f32, statistical)\n");
             std::exit(0);
         }
     }
@@ -87,7 +98,21 @@ int main(int argc, char **argv) {
             b.cam.width(), b.cam.height(), cfg.sample_sqrt * cfg.sample_sqrt, b.cam.d.max_depth);
         rtw_stats st{};
         const auto t0 = std::chrono::steady_clock::now();
-        rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st);
+        if (cfg.fast) {
+            rtw::FlatScene flat;
+            b.world->flatten(flat);
+            std::vector<float> f32(static_cast<size_t>(b.cam.width()) * b.cam.height() * 3);
+            int rc = rtw_threaded_render_fast(&b.cam.d, flat.spheres.data(),
+                                              static_cast<uint32_t>(flat.spheres.size()), flat.materials.data(),
+                                              static_cast<uint32_t>(flat.materials.size()), cfg.sample_sqrt,
+                                              seed, nullptr, f32.data(), &st);
+            if (rc != RTW_OK) throw rtw::Error(rc, rtw_last_error());
+            const std::vector<double> fb(f32.begin(), f32.end());
+            rc = rtw_write_ppm(cfg.out.c_str(), fb.data(), b.cam.width(), b.cam.height());
+            if (rc != RTW_OK) throw rtw::Error(rc, rtw_last_error());
+        } else {
+            rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st);
+        }
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::printf("Finished succesfully: %s (%.3f s wall, kernel %.3f ms, %.1f Msamples/s, seed %llu)\n",
                     cfg.out.c_str(), s, st.kernel_ms, st.samples / st.kernel_ms / 1e3, cfg.seed);

@@ -34,14 +34,15 @@ struct FastParams {
     unsigned long long *counters;  // [0] segments, [1] node visits, [2] pixels written
 };
 
-constexpr uint32_t kBlock = 512;   // 8 waves per workgroup
+constexpr uint32_t kBlock = 512;   // 8 waves per workgroup, two per CU (LDS-bound: 640 measured 25% slower)
 constexpr uint32_t kMaxStack = 32;  // per-lane BVH stack cap (u16 node ids)
 constexpr uint32_t kLdsCap = 79 * 1024;  // two workgroups per CU (160 KB), with the static ring sums
 
 // Stack slots a walk of a BVH of this depth needs: 3 pending siblings per level
-// + the top write (the root is level 0), rounded up to 8 so the scene tables
-// after the stacks stay 16-byte aligned. Deeper trees than kMaxStack allows scan.
-constexpr uint32_t stack_slots(uint32_t depth) { return (3 * depth + 2 + 7) / 8 * 8; }
+// + the top write (the root is level 0). Deeper trees than kMaxStack allows scan.
+// The scene tables follow the stacks: n_stack x kBlock x 2 bytes stays 16-aligned.
+static_assert(kBlock % 8 == 0, "stack area alignment");
+constexpr uint32_t stack_slots(uint32_t depth) { return 3 * depth + 2; }
 
 // Dynamic LDS bytes of a launch: the stacks, plus the scene tables when they fit
 // (*scene_in_lds); otherwise the kernel reads the scene from global memory.

@@ -1,0 +1,48 @@
+"""rtw_cli (the host driver mirroring main.rs, flags main.rs:32-87): one run per
+mode. Parity mode writes the PPM the oracle writes for the same flags, byte for
+byte; fast mode writes a well-formed PPM of the same size, statistically equal
+(tests/test_gpu_fast.py holds the statistics)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import raytracing_in_a_weekend_rust_amd as rtw
+from oracle import oracle_ctypes as orc
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(os.path.dirname(rtw.LIB_PATH), "rtw_cli")
+SEED = 1764892800123
+
+
+def run_cli(tmp_path, *flags):
+    out = tmp_path / "img.ppm"
+    r = subprocess.run([CLI, "-h", "18", "-w", "32", "-s", "3", "-d", "12", "--seed", str(SEED),
+                        "--out", str(out), *flags], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return out.read_bytes(), r.stdout
+
+
+def test_cli_parity_ppm_matches_oracle(tmp_path):
+    ppm, stdout = run_cli(tmp_path)
+    assert "Finished succesfully" in stdout  # main.rs's own message, spelling included
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 18, 32, 12)
+    ref, _ = orc.render(cam.raw, sph, n, mt, nm, 3, SEED)
+    assert ppm == orc.format_ppm(ref)
+
+
+def test_cli_fast_mode_ppm(tmp_path):
+    ppm, _ = run_cli(tmp_path, "--mode", "fast")
+    head, body = ppm.split(b"\n", 3)[:3], ppm.split(b"\n", 3)[3]
+    assert head == [b"P3", b"32 18", b"255"]
+    vals = np.array(body.split(), dtype=np.int64)
+    assert vals.size == 32 * 18 * 3 and vals.min() >= 0 and vals.max() <= 255 and vals.mean() > 60
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 18, 32, 12)
+    fb, _ = rtw.render_flat_fast(cam.raw, sph, n, mt, nm, 3, SEED)
+    assert ppm == rtw.format_ppm(fb.astype(np.float64))
+
+
+def test_cli_rejects_bad_mode(tmp_path):
+    r = subprocess.run([CLI, "--mode", "turbo"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "--mode" in r.stderr
