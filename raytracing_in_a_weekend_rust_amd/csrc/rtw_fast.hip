@@ -13,6 +13,8 @@
 //     (global pixel, lattice sample) seeded by SplitMix64's finaliser, instead of
 //     one XorShift chain per pixel (random.rs:33-69). A pixel's samples are
 //     independent, so one wave traces 64 of them at once;
+//   * random_unit_vec and the unit-disk sample draw their distributions directly
+//     (no rejection loop, whose retries diverge across a wave);
 //   * the pixel mean is summed in 32.32 fixed point (LDS u64 atomics): exact and
 //     order-free, so a render is deterministic and any shard reproduces the
 //     unsharded pixels bit-for-bit. Per-sample colours are clamped to [0, cmax]
@@ -69,15 +71,19 @@ __device__ __forceinline__ float rcoord(Rng &r) {
 __device__ __forceinline__ float r01(Rng &r) {
     return static_cast<float>(rnext(r) >> 8) * 5.9604644775390625e-08f;  // 2^-24
 }
-// random_unit_vec (vec3.rs:219-232): rejection with len^2 <= 1, then unit()
+// random_unit_vec (vec3.rs:219-232) draws uniformly on the unit sphere by rejection;
+// fast mode draws the same distribution directly (z uniform in [-1, 1], azimuth
+// uniform: Archimedes), with no divergent retry loop. v_sin/v_cos take revolutions.
 __device__ __forceinline__ void unit_vec(Rng &r, float &x, float &y, float &z) {
-    float l2;
-    do {
-        x = rcoord(r), y = rcoord(r), z = rcoord(r);
-        l2 = fmaf(x, x, fmaf(y, y, z * z));
-    } while (!(l2 <= 1.f && l2 > 1e-30f));
-    const float inv = __builtin_amdgcn_rsqf(l2);
-    x *= inv, y *= inv, z *= inv;
+    z = rcoord(r);
+    const float t = r01(r);
+    const float s = __builtin_sqrtf(fmaxf(fmaf(-z, z, 1.f), 0.f));
+    x = s * __builtin_amdgcn_cosf(t), y = s * __builtin_amdgcn_sinf(t);
+}
+// random_vec_in_unit_disk (vec3.rs:270-277), uniform in the open disk, directly
+__device__ __forceinline__ void disk_vec(Rng &r, float &x, float &y) {
+    const float rad = __builtin_sqrtf(r01(r)), t = r01(r);
+    x = rad * __builtin_amdgcn_cosf(t), y = rad * __builtin_amdgcn_sinf(t);
 }
 
 // A segment: origin, unit direction, t_min = 0.01 |d| in distance units.
@@ -266,11 +272,9 @@ __global__ __launch_bounds__(kBlock, 2) void rtw_fast_render(const FastParams P)
                     sz += fmaf(P.ldx[2], flx, fmaf(P.ldy[2], fly, P.pos0[2]));
                 }
                 g.ox = P.from[0], g.oy = P.from[1], g.oz = P.from[2];
-                if (P.defocus) {  // defocus_disk_sample: strict len^2 < 1 (vec3.rs:270-277)
+                if (P.defocus) {  // defocus_disk_sample (camera.rs:452-456)
                     float px, py;
-                    do {
-                        px = rcoord(rng), py = rcoord(rng);
-                    } while (!(fmaf(px, px, py * py) < 1.f));
+                    disk_vec(rng, px, py);
                     g.ox = fmaf(P.ddv[0], py, fmaf(P.ddu[0], px, g.ox));
                     g.oy = fmaf(P.ddv[1], py, fmaf(P.ddu[1], px, g.oy));
                     g.oz = fmaf(P.ddv[2], py, fmaf(P.ddu[2], px, g.oz));
