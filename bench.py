@@ -262,8 +262,7 @@ def main():
                       "brute_segments": st.brute_segments, "lds_bytes": st.lds_bytes,
                       "parked_pixels": st.parked_pixels,
                       "segments": st.segments, "segments_per_sample": round(st.segments / max(1, st.samples), 4),
-                      "lane_utilization": (round(st.segments / max(1, 64 * st.wave_iterations), 4)
-                                           if not fast else None),
+                      "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
                       "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),

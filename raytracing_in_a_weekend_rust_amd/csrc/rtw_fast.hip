@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kBlock, 2) void rtw_fast_render(const FastParams P)
     float tr = 0.f, tg = 0.f, tb = 0.f;
     uint32_t depth = 0, slot = kFree;
     Rng rng{1u, 0u};
-    uint32_t segs = 0, visits = 0, written = 0;
+    uint32_t segs = 0, visits = 0, written = 0, iters = 0;
     for (;;) {
         // ---- hand out samples of the newest pixel to idle lanes
         for (;;) {
@@ -294,6 +294,7 @@ __global__ __launch_bounds__(kBlock, 2) void rtw_fast_render(const FastParams P)
                 if (s == cs) outst[s] += took;
         }
         if (__ballot(slot != kFree) == 0) break;  // nothing handed out: the image is done
+        ++iters;
 
         // ---- one segment per busy lane (camera.rs:376-398)
         bool fin = false;
@@ -400,6 +401,7 @@ __global__ __launch_bounds__(kBlock, 2) void rtw_fast_render(const FastParams P)
         atomicAdd(P.counters + 0, sg);
         atomicAdd(P.counters + 1, vs);
         atomicAdd(P.counters + 2, static_cast<unsigned long long>(written));
+        atomicAdd(P.counters + 3, static_cast<unsigned long long>(iters));
     }
 }
 
@@ -415,7 +417,7 @@ size_t lds_bytes(uint32_t n_sph, uint32_t n_node, uint32_t n_stack, bool *scene_
 
 hipError_t launch(const FastParams &P, int n_cu, hipStream_t st) {
     hipError_t e = hipMemsetAsync(P.cursor, 0, sizeof(uint32_t), st);
-    if (e == hipSuccess) e = hipMemsetAsync(P.counters, 0, 3 * sizeof(unsigned long long), st);
+    if (e == hipSuccess) e = hipMemsetAsync(P.counters, 0, 4 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     if (P.n_rows == 0 || P.W == 0) return hipSuccess;
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;

@@ -2310,12 +2310,13 @@ void collect(rtw_session *s) {
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
     if (s->last_fast) {
-        unsigned long long c[3] = {};
+        unsigned long long c[4] = {};
         HIPCHECK(hipMemcpy(c, s->d_fcount, sizeof c, hipMemcpyDeviceToHost));
         float ms = 0.f;
         HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         s->last.segments = c[0];
         s->last.node_visits = c[1];
+        s->last.wave_iterations = c[3];
         s->last.sphere_tests = c[0] * s->n_sph;
         s->last.kernel_ms = ms;
         s->pending = false;
