@@ -6,7 +6,7 @@ This renders every rank's shard (or the first `--ranks`) on cuda:0 and prints
 the kernel times, the implied whole-job Msamples/s and the strong-scaling
 efficiency against N=1.
 
-usage: python tools/shard_time.py [N ...]   (default 1 2 4 8)
+usage: python tools/shard_time.py [--fast] [N ...]   (default 1 2 4 8; --fast: f32 mode)
 """
 import os
 import sys
@@ -22,7 +22,9 @@ SEED = rtw.DEFAULT_SEED
 
 
 def main():
-    ns_list = [int(x) for x in sys.argv[1:]] or [1, 2, 4, 8]
+    args = sys.argv[1:]
+    fast = "--fast" in args
+    ns_list = [int(x) for x in args if x != "--fast"] or [1, 2, 4, 8]
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, H, W, DEPTH)
     sess = rtw.Session(0)
     sess.set_scene(sph, n, mt, nm)
@@ -30,7 +32,8 @@ def main():
     base = None
     for N in ns_list:
         rm = shard.rows_max(N, H)
-        fb = torch.zeros((rm, W, 3), dtype=torch.float64, device="cuda:0")
+        fb = torch.zeros((rm, W, 3), dtype=torch.float32 if fast else torch.float64, device="cuda:0")
+        render = sess.render_fast if fast else sess.render
         times = []
         for r in range(N):
             rb, rstep, rows = shard.rows_of(r, N, H)
@@ -39,8 +42,8 @@ def main():
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                sess.render(cam.raw, S, SEED, fb.data_ptr(), stream=stream.cuda_stream,
-                            shard=(rb, rstep, rows))
+                render(cam.raw, S, SEED, fb.data_ptr(), stream=stream.cuda_stream,
+                       shard=(rb, rstep, rows))
                 e1.record(stream)
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1)
