@@ -52,7 +52,10 @@ constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
 constexpr int kCounters = 10;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
-constexpr uint32_t kTailSegs = 768;     // dry-cursor parking: estimated segments left (RTW_TAIL)
+// dry-cursor parking: estimated segments left (RTW_TAIL), per lattice sample of the
+// pixel: 768 at 529 spp (tuned there); 145 at 100 spp and 2940 at 2025 spp measured
+// better than a fixed 768 (38.1 -> 36.1 ms; 1026 -> 864 ms per rank of 8 at 4096x2304)
+constexpr double kTailSegsPerSample = 768. / 529.;
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
@@ -2183,7 +2186,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // waves that signal the end of their cursor loop: priority waves too when they join
         P.n_cursor_waves = P.join_at != 0xffffffffu ? grid_p * wpb : grid_p * (wpb - heavy);
         P.rate_k = 16, P.rate_x = 16;
-        P.tail_segs = small_shard ? 0xffffffffu : kTailSegs;
+        P.tail_segs = small_shard ? 0xffffffffu
+                                  : static_cast<uint32_t>(std::max(64., std::round(kTailSegsPerSample * P.n_off)));
         if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));

@@ -275,6 +275,18 @@ def test_final_scene_config4_sampled_rows():
     assert_same(fb, ref, st, seg)
 
 
+def test_stress_config5_sampled_rows():
+    """BASELINE stress config (4096x2304, spp 2000 -> s=45, depth 50): the largest
+    image -- 9.4M pixels, 24-bit jump-ahead -- on one sampled row, bit-exact vs
+    the oracle."""
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 2304, 4096, 50)
+    rows = (2047, 256, 1)  # image row 2047 (ground, near the bottom)
+    fb, st = gpu(cam, sph, n, mt, nm, 45, SEED, shard=rows)
+    assert st.samples == 4096 * 2025
+    ref, seg = oracle(cam, sph, n, mt, nm, 45, SEED, rows=rows)
+    assert_same(fb, ref, st, seg)
+
+
 def test_deep_paths_use_spill_levels():
     """Camera inside a closed Lambertian sphere: every path bounces to the depth
     cap, so the path stack runs past its register slots into the HBM spill levels."""
