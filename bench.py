@@ -265,6 +265,9 @@ def main():
                       "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
                       "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
+                      **({"walk_wave_iters_per_wave_iteration": round(st.exact_wave_iterations /
+                                                                      max(1, st.wave_iterations), 3)}
+                         if fast else {}),
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),
                       "trap_skipped_fraction": round(st.trap_segments / max(1, st.segments), 4)},
         }

@@ -87,7 +87,9 @@ typedef struct rtw_stats {
     uint64_t sphere_tests;    /* segments x n_spheres (brute force, as the reference)  */
     uint64_t wave_iterations; /* sum over waves of the wave's loop trip count          */
     uint64_t exact_tests;     /* f64 sphere tests run after the conservative filter    */
-    uint64_t exact_wave_iterations; /* wave-level iterations of the exact-test loop    */
+    uint64_t exact_wave_iterations; /* wave-level iterations of the exact-test loop
+                                       (fast mode: of the BVH walk loop, diagnostic
+                                       builds with -DRTW_FAST_DIAG; else 0)           */
     double kernel_ms;         /* render kernel time, HIP events on the launch stream   */
     uint32_t grid_blocks, block_threads;
     uint64_t node_visits;     /* BVH walk iterations (inner-node or leaf tests), lanes  */

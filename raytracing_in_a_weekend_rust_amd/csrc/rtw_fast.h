@@ -31,7 +31,8 @@ struct FastParams {
     const uint32_t *always; // spheres tested before the walk (rtw_accel.h)
     float *out;             // n_rows x W x 3 f32
     uint32_t *cursor;       // pixel hand-out counter (zeroed by the launcher)
-    unsigned long long *counters;  // [0] segments, [1] node visits, [2] pixels written, [3] wave iterations
+    unsigned long long *counters;  // [0] segments, [1] node visits, [2] pixels written, [3] wave iterations,
+                                   // [4] wave-level walk iterations
 };
 
 constexpr uint32_t kBlock = 512;   // 8 waves per workgroup, two per CU (LDS-bound: 640 measured 25% slower)

@@ -2314,13 +2314,14 @@ void collect(rtw_session *s) {
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
     if (s->last_fast) {
-        unsigned long long c[4] = {};
+        unsigned long long c[5] = {};
         HIPCHECK(hipMemcpy(c, s->d_fcount, sizeof c, hipMemcpyDeviceToHost));
         float ms = 0.f;
         HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         s->last.segments = c[0];
         s->last.node_visits = c[1];
         s->last.wave_iterations = c[3];
+        s->last.exact_wave_iterations = c[4];  // fast mode: wave-level walk iterations (RTW_FAST_DIAG builds)
         s->last.sphere_tests = c[0] * s->n_sph;
         s->last.kernel_ms = ms;
         s->pending = false;
@@ -2373,7 +2374,7 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_cost_hist, kCostBuckets * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_fcursor, sizeof(uint32_t)));
-        HIPCHECK(hipMalloc(&s->d_fcount, 4 * sizeof(unsigned long long)));
+        HIPCHECK(hipMalloc(&s->d_fcount, 8 * sizeof(unsigned long long)));
         HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));
         upload_jump(s);
     } catch (...) {
