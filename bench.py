@@ -70,9 +70,33 @@ def parse():
                    help="parity = f64 bit-exact (the headline); fast = the f32 mode with "
                         "independent per-sample streams (statistical parity, tests/test_gpu_fast.py)")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU leg")
+    p.add_argument("--e2e", type=int, default=1,
+                   help="0 disables the end-to-end leg (one-shot ABI call with host buffers + PPM)")
     p.add_argument("--cpu-row-stride", type=int, default=0,
                    help="oracle renders every k-th row (0 = auto, ~10-30 s)")
     return p.parse_args()
+
+
+def end_to_end(cam, sph, ns, mt, nm, s, seed, fast, kernel_ms):
+    """SURVEY.md 8(d)'s end-to-end figure, outside the timed region: the one-shot
+    rtw_threaded_render(_fast) (scene upload, seeds, render, framebuffer download to a
+    host buffer: the reference's Camera::threaded_render, camera.rs:223-352) and then
+    the PPM text (Color::wire_full_file, color.rs:196-247). One untimed call first
+    (device context, allocations), then one timed call."""
+    one_shot = rtw.render_flat_fast if fast else rtw.render_flat
+    one_shot(cam, sph, ns, mt, nm, s, seed)
+    t0 = time.perf_counter()
+    fb, _ = one_shot(cam, sph, ns, mt, nm, s, seed)
+    t1 = time.perf_counter()
+    ppm = rtw.format_ppm(fb)
+    t2 = time.perf_counter()
+    render_ms, ppm_ms = (t1 - t0) * 1e3, (t2 - t1) * 1e3
+    samples = W * H * (s * s if s else 1)
+    return {"render_ms": round(render_ms, 3), "ppm_ms": round(ppm_ms, 3), "ppm_bytes": len(ppm),
+            "host_overhead_ms": round(render_ms - kernel_ms, 3),
+            "value": round(samples / ((render_ms + ppm_ms) / 1e3) / 1e6, 3), "unit": "Msamples/s",
+            "note": "one-shot ABI call with host buffers (PCIe upload/download, seeds, render) + PPM "
+                    "text; host_overhead_ms = render_ms - resident kernel_ms. Not `value`"}
 
 
 def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
@@ -271,6 +295,8 @@ def main():
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),
                       "trap_skipped_fraction": round(st.trap_segments / max(1, st.segments), 4)},
         }
+    if rank == 0 and world == 1 and a.e2e:
+        out["end_to_end"] = end_to_end(cam.raw, sph, ns, mt, nm, s, render_seed, fast, kms)
     if rank == 0 and world == 1 and a.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)
         out["cpu_baseline"]["gpu_speedup"] = round(value / out["cpu_baseline"]["value"], 1)

@@ -215,9 +215,14 @@ def format_ppm(fb: np.ndarray) -> bytes:
     fb = np.ascontiguousarray(fb, dtype=np.float64)
     h, w = fb.shape[0], fb.shape[1]
     p = fb.ctypes.data_as(C.POINTER(C.c_double))
-    n = check(lib.rtw_format_ppm(p, w, h, None, 0))
-    buf = C.create_string_buffer(n)
-    check(lib.rtw_format_ppm(p, w, h, buf, n))
+    # one formatting pass in the common case: values in [0, 1] give <= 4 bytes a
+    # channel; the size query + second call only when a brighter image overflows
+    cap = 12 * w * h + h + 64
+    buf = C.create_string_buffer(cap)
+    n = check(lib.rtw_format_ppm(p, w, h, buf, cap))
+    if n > cap:
+        buf = C.create_string_buffer(n)
+        check(lib.rtw_format_ppm(p, w, h, buf, n))
     return buf.raw[:n]
 
 

@@ -317,9 +317,13 @@ static void format_rows(const double *rgb, uint32_t w, uint32_t y0, uint32_t y1,
         const double *row = rgb + static_cast<size_t>(y) * w * 3;
         for (uint64_t i = 0; i < 3ull * w; ++i) {
             const double g = std::pow(row[i], 1. / 2.2);  // gamma_correct, color.rs:241-247
-            const int l = std::snprintf(tmp, sizeof tmp, "%llu",
-                                        static_cast<unsigned long long>(sat_u64(g * 255.)));
-            s.append(tmp, static_cast<size_t>(l));
+            uint64_t v = sat_u64(g * 255.);
+            char *e = tmp + sizeof tmp, *b = e;  // decimal digits, right to left
+            do {
+                *--b = static_cast<char>('0' + v % 10u);
+                v /= 10u;
+            } while (v);
+            s.append(b, static_cast<size_t>(e - b));
             s.push_back(i + 1 == 3ull * w ? '\n' : ' ');
         }
     }

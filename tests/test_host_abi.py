@@ -140,6 +140,15 @@ def test_ppm_writer_edge_values_and_parallel_rows():
     assert rtw.format_ppm(fb) == orc.format_ppm(fb)
 
 
+def test_ppm_writer_bright_image_outgrows_first_buffer():
+    # > 4 bytes per channel: the Python mirror's first buffer is too small and it
+    # retries at the size the ABI reports
+    rng = np.random.default_rng(4)
+    fb = rng.random((40, 30, 3)) * 1e4
+    fb[1, 2] = [math.inf, 1e300, 3.0]
+    assert rtw.format_ppm(fb) == orc.format_ppm(fb)
+
+
 def test_reference_asserts_become_error_codes():
     with pytest.raises(rtw.RtwError) as e:
         rtw.Metal((0.5, 0.5, 0.5), 1.01)  # materials.rs:47
