@@ -223,7 +223,7 @@ def format_ppm(fb: np.ndarray) -> bytes:
     if n > cap:
         buf = C.create_string_buffer(n)
         check(lib.rtw_format_ppm(p, w, h, buf, n))
-    return buf.raw[:n]
+    return C.string_at(buf, n)
 
 
 def write_ppm(path: str, fb: np.ndarray):

@@ -330,23 +330,31 @@ static void format_rows(const double *rgb, uint32_t w, uint32_t y0, uint32_t y1,
 }
 // color.rs:196-239. Rows are formatted in parallel chunks (the reference's
 // single-threaded fold is the output edge's cost at 4096x2304).
-std::string format_ppm(const double *rgb, uint32_t w, uint32_t h) {
-    std::string head = "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+std::vector<std::string> format_ppm_parts(const double *rgb, uint32_t w, uint32_t h) {
     unsigned nt = std::thread::hardware_concurrency();
     nt = nt ? (nt > 16 ? 16 : nt) : 1;
     if (static_cast<uint64_t>(w) * h < 65536) nt = 1;
-    std::vector<std::string> parts(nt);
+    std::vector<std::string> parts(nt + 1);
+    parts[0] = "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t) {
         const uint32_t y0 = static_cast<uint32_t>(static_cast<uint64_t>(h) * t / nt);
         const uint32_t y1 = static_cast<uint32_t>(static_cast<uint64_t>(h) * (t + 1) / nt);
-        parts[t].reserve(static_cast<size_t>(y1 - y0) * w * 12);
-        if (t + 1 == nt) format_rows(rgb, w, y0, y1, parts[t]);
-        else th.emplace_back(format_rows, rgb, w, y0, y1, std::ref(parts[t]));
+        std::string &part = parts[t + 1];
+        auto work = [=, &part] {
+            part.reserve(static_cast<size_t>(y1 - y0) * w * 12);  // allocated in the worker
+            format_rows(rgb, w, y0, y1, part);
+        };
+        if (t + 1 == nt) work();
+        else th.emplace_back(work);
     }
     for (auto &x : th) x.join();
-    for (auto &p : parts) head += p;
-    return head;
+    return parts;
+}
+std::string format_ppm(const double *rgb, uint32_t w, uint32_t h) {
+    std::string s;
+    for (const auto &p : format_ppm_parts(rgb, w, h)) s += p;
+    return s;
 }
 
 }  // namespace rtw
@@ -445,9 +453,12 @@ int64_t rtw_format_ppm(const double *rgb, uint32_t width, uint32_t height, char 
                        uint64_t cap) {
     if (!rgb && width && height) return set_error("null argument"), RTW_E_ARG;
     try {
-        const std::string s = format_ppm(rgb, width, height);
-        if (buf && cap >= s.size()) std::memcpy(buf, s.data(), s.size());
-        return static_cast<int64_t>(s.size());
+        const auto parts = format_ppm_parts(rgb, width, height);
+        size_t n = 0;
+        for (const auto &p : parts) n += p.size();
+        if (buf && cap >= n)
+            for (const auto &p : parts) std::memcpy(buf, p.data(), p.size()), buf += p.size();
+        return static_cast<int64_t>(n);
     } catch (const std::exception &e) {
         set_error(e.what());
         return RTW_E_ARG;
@@ -458,12 +469,13 @@ int rtw_write_ppm(const char *path, const double *rgb, uint32_t width, uint32_t 
     if (!path || (!rgb && width && height)) return set_error("null argument"), RTW_E_ARG;
     if (width == 0 || height == 0) return set_error("empty image"), RTW_E_EMPTY_IMAGE;
     RTW_GUARD_BEGIN
-    const std::string s = format_ppm(rgb, width, height);
+    const auto parts = format_ppm_parts(rgb, width, height);
     FILE *f = std::fopen(path, "wb");
     if (!f) return set_error(std::string("cannot create ") + path), RTW_E_ARG;
-    const size_t n = std::fwrite(s.data(), 1, s.size(), f);
+    bool short_write = false;
+    for (const auto &p : parts) short_write |= std::fwrite(p.data(), 1, p.size(), f) != p.size();
     const int rc = std::fclose(f);
-    if (n != s.size() || rc != 0) return set_error("short write"), RTW_E_ARG;
+    if (short_write || rc != 0) return set_error("short write"), RTW_E_ARG;
     return RTW_OK;
     RTW_GUARD_END
 }

@@ -160,6 +160,8 @@ BuiltScene build_scene(const std::string &name, rtw_u128 seed, uint32_t h, uint3
 
 // ---- output (color.rs:196-247) ----
 std::string format_ppm(const double *rgb, uint32_t w, uint32_t h);
+// the same text as the header followed by row-block chunks (no concatenation)
+std::vector<std::string> format_ppm_parts(const double *rgb, uint32_t w, uint32_t h);
 
 // Error carrying an RTW_E_* code (mapped to the C ABI's return value).
 struct Error : std::runtime_error {
