@@ -114,10 +114,21 @@ def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
                         nthreads=threads, scheduler=0)
     dt = time.perf_counter() - t0
     samples = n_rows * cam.img_width * (s * s if s else 1)
+    # also the "clean" scheduler (rows pulled by the workers, direct
+    # calls, no per-pixel job/refcount overhead), on the same sampled rows
+    c_stride = stride
+    c_rows = len(range(0, cam.img_height, c_stride))
+    t0 = time.perf_counter()
+    orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, c_stride, c_rows), nthreads=threads, scheduler=1)
+    c_dt = time.perf_counter() - t0
+    c_samples = c_rows * cam.img_width * (s * s if s else 1)
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"rows 0::{stride} ({n_rows} rows x {cam.img_width} px x {s * s} spp, "
                       f"{samples / 1e6:.1f} Msamples) of the same image, {dt:.1f} s, "
-                      f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible"}
+                      f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible",
+            "clean_scheduler": {"value": c_samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
+                                "sample": f"rows 0::{c_stride} ({c_rows} rows), {c_dt:.1f} s, row jobs, "
+                                          "direct calls"}}
 
 
 def main():
@@ -300,6 +311,8 @@ def main():
     if rank == 0 and world == 1 and a.cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)
         out["cpu_baseline"]["gpu_speedup"] = round(value / out["cpu_baseline"]["value"], 1)
+        cl = out["cpu_baseline"]["clean_scheduler"]
+        cl["gpu_speedup"] = round(value / cl["value"], 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     sess.close()
