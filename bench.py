@@ -99,13 +99,45 @@ def end_to_end(cam, sph, ns, mt, nm, s, seed, fast, kernel_ms):
                     "text; host_overhead_ms = render_ms - resident kernel_ms. Not `value`"}
 
 
+def available_parallelism():
+    """What the reference's pool would size itself to: Camera::threaded_render uses
+    ThreadPoolBuilder::with_max_threads() (camera.rs:253) = Rust's
+    std::thread::available_parallelism(), which on Linux is the CPU-affinity count
+    capped by the cgroup CPU quota (cgroup v2 cpu.max, or v1 cfs_quota/period).
+    Returns (threads, how it was derived)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    n = min(aff, quota) if quota else aff
+    how = (f"available_parallelism(): min(affinity {aff}, cgroup CPU quota {quota})" if quota
+           else f"available_parallelism(): affinity {aff} (no cgroup CPU quota)")
+    return n, how
+
+
 def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
     """Oracle (C restatement) on a row sample, ref-faithful scheduler: one job per
     pixel pulled by `threads` workers, dyn dispatch + Arc-refcount traffic as in
     camera.rs:269-292 / sphere.rs:69."""
     from oracle import oracle_ctypes as orc  # test infrastructure: checker/baseline only
 
-    threads = min(16, os.cpu_count() or 1)
+    # the reference's own pool size on this host (not a cap of ours)
+    threads, how = available_parallelism()
+    if os.environ.get("RTW_CPU_THREADS"):
+        threads, how = int(os.environ["RTW_CPU_THREADS"]), "RTW_CPU_THREADS override"
     if stride <= 0:  # ~4 rows per thread: ~15 s of CPU work at ~0.16 Msamples/s/core
         stride = max(1, int(round(cam.img_height / (4 * threads))))
     n_rows = len(range(0, cam.img_height, stride))
@@ -126,6 +158,7 @@ def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
             "sample": f"rows 0::{stride} ({n_rows} rows x {cam.img_width} px x {s * s} spp, "
                       f"{samples / 1e6:.1f} Msamples) of the same image, {dt:.1f} s, "
                       f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible",
+            "threads_rule": how,
             "clean_scheduler": {"value": c_samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
                                 "sample": f"rows 0::{c_stride} ({c_rows} rows), {c_dt:.1f} s, row jobs, "
                                           "direct calls"}}

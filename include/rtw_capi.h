@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 4
+#define RTW_ABI_VERSION 5
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -99,6 +99,11 @@ typedef struct rtw_stats {
     uint64_t parked_pixels;   /* pixels finished by the cooperative second kernel      */
     uint64_t inside_segments; /* segments resolved by the inside cut (rtw_accel.h)     */
     uint64_t trap_segments;   /* segments skipped by the trapped-path fast-forward      */
+    /* ABI 5: */
+    uint64_t guard_exits;     /* idle waits of the persistent kernel ended by its
+                                 no-progress guard ($RTW_SPIN_GUARD_MS, default 100)   */
+    uint64_t leftover_pixels; /* parked pixels finished by the follow-up launch (after
+                                 guard exits; 0 on an exclusive device)                 */
 } rtw_stats;
 
 /* ---- library ---- */
@@ -175,7 +180,19 @@ int rtw_session_set_scene(rtw_session *s, const rtw_sphere *spheres, uint32_t n_
                           const rtw_material *mats, uint32_t n_mats);
 /* Asynchronous: enqueues the render of `shard` on `hip_stream` (a hipStream_t;
  * NULL = HIP's null stream, as everywhere in HIP) writing out_rgb_device (device
- * pointer, n_rows*W*3 f64). */
+ * pointer, n_rows*W*3 f64).
+ * Concurrency: all renders of one session share its device buffers, so at most
+ * one runs at a time -- a render enqueued on a different stream than the
+ * session's previous render waits for it (hipStreamWaitEvent). Use one session
+ * per concurrent render. Completeness (one write per pixel) is checked on the
+ * device after EVERY render and latched: rtw_session_stats fails if any render
+ * since its previous call was incomplete, even if later renders were enqueued
+ * before it was called.
+ * Residency: the persistent kernel (one workgroup per CU) is fastest with the
+ * device to itself, but never depends on all of its workgroups being resident at
+ * once: waves that wait for parked pixels leave after $RTW_SPIN_GUARD_MS (default
+ * 100) without progress anywhere, and a follow-up launch finishes any parked
+ * pixel they left (rtw_stats.guard_exits / leftover_pixels). */
 int rtw_session_render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt,
                        rtw_u128 seed, const rtw_shard *shard, double *out_rgb_device,
                        void *hip_stream);

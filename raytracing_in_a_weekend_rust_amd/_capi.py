@@ -72,7 +72,8 @@ class Stats(C.Structure):
                 ("block_threads", C.c_uint32), ("node_visits", C.c_uint64),
                 ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("parked_pixels", C.c_uint64), ("inside_segments", C.c_uint64),
-                ("trap_segments", C.c_uint64)]
+                ("trap_segments", C.c_uint64), ("guard_exits", C.c_uint64),
+                ("leftover_pixels", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

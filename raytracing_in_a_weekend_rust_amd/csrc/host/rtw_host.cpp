@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <exception>
 #include <thread>
 
 #include "rtw_internal.h"
@@ -336,19 +337,39 @@ std::vector<std::string> format_ppm_parts(const double *rgb, uint32_t w, uint32_
     if (static_cast<uint64_t>(w) * h < 65536) nt = 1;
     std::vector<std::string> parts(nt + 1);
     parts[0] = "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+    // Exception safety: a worker's exception (bad_alloc of a ~100 MB part) is
+    // caught into its slot and rethrown after every thread has joined; the joiner
+    // also runs when this thread throws (thread creation, its own chunk), so no
+    // joinable std::thread is ever destroyed (which would std::terminate).
+    std::vector<std::exception_ptr> errs(nt);
     std::vector<std::thread> th;
+    struct Joiner {
+        std::vector<std::thread> &t;
+        ~Joiner() {
+            for (auto &x : t)
+                if (x.joinable()) x.join();
+        }
+    } joiner{th};
+    th.reserve(nt);
     for (unsigned t = 0; t < nt; ++t) {
         const uint32_t y0 = static_cast<uint32_t>(static_cast<uint64_t>(h) * t / nt);
         const uint32_t y1 = static_cast<uint32_t>(static_cast<uint64_t>(h) * (t + 1) / nt);
         std::string &part = parts[t + 1];
-        auto work = [=, &part] {
-            part.reserve(static_cast<size_t>(y1 - y0) * w * 12);  // allocated in the worker
-            format_rows(rgb, w, y0, y1, part);
+        std::exception_ptr &err = errs[t];
+        auto work = [=, &part, &err] {
+            try {
+                part.reserve(static_cast<size_t>(y1 - y0) * w * 12);  // allocated in the worker
+                format_rows(rgb, w, y0, y1, part);
+            } catch (...) {
+                err = std::current_exception();
+            }
         };
         if (t + 1 == nt) work();
         else th.emplace_back(work);
     }
     for (auto &x : th) x.join();
+    for (auto &e : errs)
+        if (e) std::rethrow_exception(e);
     return parts;
 }
 std::string format_ppm(const double *rgb, uint32_t w, uint32_t h) {
@@ -376,7 +397,7 @@ using namespace rtw;
 
 extern "C" {
 
-const char *rtw_version(void) { return "rtw-mi355x 0.4.0 (abi 4, gfx950)"; }
+const char *rtw_version(void) { return "rtw-mi355x 0.5.0 (abi 5, gfx950)"; }
 const char *rtw_last_error(void) { return rtw::last_error(); }
 
 int rtw_camera_new(uint32_t img_height, uint32_t img_width, uint32_t max_depth,

@@ -50,7 +50,7 @@ constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
-constexpr int kCounters = 10;
+constexpr int kCounters = 12;
 constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
 // dry-cursor parking: estimated segments left (RTW_TAIL), per lattice sample of the
 // pixel: 768 at 529 spp (tuned there); 145 at 100 spp and 2940 at 2025 spp measured
@@ -153,10 +153,14 @@ struct KParams {
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
     uint32_t *park_flag;        // per park slot: 1 once the entry is published
     uint32_t *pixels_done;      // pixels written (completeness check of the persistent kernel)
+    uint32_t *park_processed;   // park entries finished (persistent drain + leftover launch)
+    uint32_t *leftover_cursor;  // slot cursor of the leftover launch (rtw_park_leftover)
+    uint64_t spin_guard;        // idle waits end after this many 100 MHz ticks without progress
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
                                    // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
-                                   // [6] parked pixels, [7] queue spin timeouts, [8] inside cuts,
-                                   // [9] segments skipped by the trapped-path fast-forward
+                                   // [6] parked pixels, [7] idle waits ended by the no-progress guard,
+                                   // [8] inside cuts, [9] segments skipped by the trapped-path
+                                   // fast-forward, [10] park entries left to rtw_park_leftover
 };
 
 // ------------------------------------------------------------------ XorShift --
@@ -998,6 +1002,37 @@ __global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
 __device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
     return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Idle-wait guard of the persistent kernel. A waiting lane gives up only when
+// NOTHING has progressed anywhere for P.spin_guard ticks of the 100 MHz clock:
+// no pixel handed out, finished or parked, no cursor wave retired (a sum of
+// monotonic counters changes iff one of them moved). So a long render never
+// trips it (pixels finish every few ms); a wave that does leave holds no entry
+// it alone could finish -- a ticket it claimed stays published-but-unclaimed
+// (flag 1) and the leftover launch (rtw_park_leftover) finishes it. Progress
+// therefore never depends on every workgroup being resident at once.
+__device__ __forceinline__ uint32_t progress_sig(const KParams &P) {
+    return ld_rlx(P.park_count) + ld_rlx(P.pixels_done) + ld_rlx(P.pix_cursor) + ld_rlx(P.park_ctl_done);
+}
+struct SpinGuard {
+    uint64_t t0;
+    uint32_t sig;
+    __device__ explicit SpinGuard(const KParams &P) : t0(__builtin_amdgcn_s_memrealtime()), sig(progress_sig(P)) {}
+    __device__ bool expired(const KParams &P) {
+        const uint32_t s = progress_sig(P);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (s != sig) {
+            sig = s, t0 = now;
+            return false;
+        }
+        return now - t0 > P.spin_guard;
+    }
+};
+// Park slot flags: 0 free, 1 published, 2 claimed by a group that finishes it.
+constexpr uint32_t kSlotPublished = 1u, kSlotClaimed = 2u;
+__device__ __forceinline__ void claim_slot(const KParams &P, uint32_t t) {
+    __hip_atomic_store((gu32 *)(P.park_flag + t), kSlotClaimed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void publish_parked(const KParams &P, const Parked &q) {
     const uint32_t slot = atomicAdd(P.park_count, 1u);
     const unsigned long long *w = reinterpret_cast<const unsigned long long *>(&q);
@@ -1319,12 +1354,14 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         while (P.join_at != 0xffffffffu) {
             uint32_t t = 0, state = 0;  // 1: ticket t, 2: join the cursor
             if (sub == 0) {
+                SpinGuard guard(P);
                 for (uint32_t spins = 0;; ++spins) {
                     const uint32_t c = ld_rlx(P.park_cursor), n = ld_rlx(P.park_count);
                     if (c < n) {
                         if (atomicCAS(P.park_cursor, c, c + 1u) == c) {
                             t = c;
-                            while (ld_rlx(P.park_flag + t) != 1u) __builtin_amdgcn_s_sleep(2);
+                            while (ld_rlx(P.park_flag + t) != kSlotPublished) __builtin_amdgcn_s_sleep(2);
+                            claim_slot(P, t);
                             state = 1;
                             break;
                         }
@@ -1335,9 +1372,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         break;
                     }
                     __builtin_amdgcn_s_sleep(16);
-                    if ((spins & 1023u) == 1023u &&
-                        __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
-                        atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
+                    if ((spins & 255u) == 255u && guard.expired(P)) {
+                        atomicAdd(&P.counters[7], 1ull);  // nothing moves: join the cursor
                         state = 2;
                         break;
                     }
@@ -1356,6 +1392,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+            if (sub == 0) atomicAdd(P.park_processed, 1u);
         }
         tl.seg += cseg;
     }
@@ -1599,9 +1636,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         uint32_t t = 0, state = 0;  // state 1: ticket t is published, 2: stop
         if (sub == 0) {
             t = atomicAdd(P.park_cursor, 1u);
+            SpinGuard guard(P);
             for (uint32_t spins = 0;; ++spins) {
                 if (t < ld_rlx(P.park_count)) {
-                    while (ld_rlx(P.park_flag + t) != 1u) __builtin_amdgcn_s_sleep(2);
+                    while (ld_rlx(P.park_flag + t) != kSlotPublished) __builtin_amdgcn_s_sleep(2);
+                    claim_slot(P, t);
                     state = 1;
                     break;
                 }
@@ -1612,9 +1651,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     break;
                 }
                 __builtin_amdgcn_s_sleep(16);
-                if ((spins & 1023u) == 1023u &&
-                    __builtin_amdgcn_s_memrealtime() - t_start > 100ull * 1000 * 1000 * 30) {
-                    atomicAdd(&P.counters[7], 1ull);  // 30 s: give up rather than hang
+                // nothing moves anywhere (e.g. workgroups of this launch that are not
+                // resident yet): leave; a ticket t published later stays unclaimed
+                // and the leftover launch finishes it
+                if ((spins & 255u) == 255u && guard.expired(P)) {
+                    atomicAdd(&P.counters[7], 1ull);
                     state = 2;
                     break;
                 }
@@ -1630,8 +1671,49 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+        if (sub == 0) atomicAdd(P.park_processed, 1u);
     }
     tl.seg += cseg;
+    flush_tally(P, tl, false);
+}
+
+// Leftover launch after the persistent kernel: park entries that were published
+// but never claimed -- only possible when waiting waves left on the no-progress
+// guard (SpinGuard). Exits at once in the normal case (every entry finished).
+// Kernel boundary: every entry and flag is visible with plain loads.
+template <bool kLds, uint32_t kG>
+__global__ __launch_bounds__(kBlock) void rtw_park_leftover(const KParams P) {
+    if (*P.park_processed >= *P.park_count) return;  // block-uniform
+    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
+    const float4 *filt =
+        stage_filt<kLds>(P, reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph));
+    const uint32_t sub = threadIdx.x & (kG - 1u);
+    const int gl = static_cast<int>(threadIdx.x & 63u & ~(kG - 1u));
+    Tally tl;
+    Stamps stp;
+    uint32_t seg = 0;
+    const uint32_t n = *P.park_count;
+    for (;;) {
+        uint32_t item = 0, flag = 0;
+        if (sub == 0) {
+            item = atomicAdd(P.leftover_cursor, 1u);
+            if (item < n) flag = P.park_flag[item];
+        }
+        item = __shfl(item, gl);
+        flag = __shfl(flag, gl);
+        if (item >= n) break;
+        if (flag != kSlotPublished) continue;  // finished by the persistent kernel
+        const Parked q = P.park[item];
+        // spill columns: region B, column = slot (the persistent kernel's groups
+        // used group-base columns; a kernel boundary separates the two uses)
+        seg += coop_pixel<kG>(P, sv, filt, q, item, tl, stp);
+        if (sub == 0) {
+            atomicAdd(&P.counters[10], 1ull);
+            atomicAdd(P.park_processed, 1u);
+        }
+    }
+    tl.seg = seg;
     flush_tally(P, tl, false);
 }
 
@@ -1663,6 +1745,15 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
 #endif
     tl.seg = seg;
     flush_tally(P, tl, false);
+}
+
+// Completeness latch, enqueued after every render: an image with fewer pixel
+// writes than pixels bumps the session's error word, which stays set until
+// rtw_session_stats reads it -- so a failed render is reported even when the
+// caller enqueued the next render before asking for stats.
+template <typename T>
+__global__ void rtw_latch_check(const T *written, T expect, uint32_t *err) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && *written != expect) atomicAdd(err, 1u);
 }
 
 // ------------------------------------------------------------------- probes --
@@ -1732,6 +1823,7 @@ struct rtw_session {
     unsigned long long *d_fcount = nullptr;
     bool last_fast = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    uint32_t *d_err = nullptr;  // latched count of incomplete renders (rtw_latch_check)
     hipStream_t last_stream = nullptr;
     bool pending = false;
     rtw_stats last{};
@@ -1930,6 +2022,13 @@ uint64_t *&stamp_buf() { static uint64_t *p = nullptr; return p; }
 size_t &stamp_n() { static size_t n = 0; return n; }
 #endif
 
+// Every render of a session shares its buffers (counters, park queue, seeds,
+// spill): a render enqueued on another stream than the previous one first waits
+// for it, so at most one render per session runs at a time.
+void order_after_last(rtw_session *s, hipStream_t st) {
+    if (s->pending && s->last_stream != st) HIPCHECK(hipStreamWaitEvent(st, s->ev1, 0));
+}
+
 void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
             const rtw_shard *shard_in, double *out, hipStream_t stream) {
     if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
@@ -2036,6 +2135,14 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.pix_cursor = s->d_park_ctl + 2;
     P.park_ctl_done = s->d_park_ctl + 3;
     P.pixels_done = s->d_park_ctl + 4;
+    P.park_processed = s->d_park_ctl + 5;
+    P.leftover_cursor = s->d_park_ctl + 6;
+    {
+        // idle-wait guard (SpinGuard): RTW_SPIN_GUARD_MS of no progress anywhere
+        double ms = 100.;
+        if (const char *e = std::getenv("RTW_SPIN_GUARD_MS")) ms = std::atof(e);
+        P.spin_guard = static_cast<uint64_t>(std::max(0., ms) * 1e5);  // 100 MHz ticks
+    }
     P.park_flag = s->d_park_flag;
     P.seeds = s->d_seeds;
     {
@@ -2084,6 +2191,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
 
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
+    order_after_last(s, st);
     const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
     // Scene::hit strategy: RTW_ACCEL=0 f64 scan, 1 filtered scan, 2 BVH (default
     // when the scene is eligible); A/B and tests only -- results are identical.
@@ -2195,6 +2303,12 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};
         HIPCHECK(hipLaunchKernel(fn, dim3(grid_p), dim3(pblock), args, lds, st));
+        // entries no group claimed (only after guard exits); returns at once otherwise
+        const size_t lds2 = lds_bytes_for(P.n_sph, 0, 0, false) + static_cast<size_t>(P.n_sph) * sizeof(float4);
+        const dim3 grid_l(static_cast<uint32_t>(s->n_cu > 0 ? s->n_cu : 256));
+        if (lds2 <= kLdsCap) hipLaunchKernelGGL((rtw_park_leftover<true, 64>), grid_l, dim3(kBlock), lds2, st, P);
+        else hipLaunchKernelGGL((rtw_park_leftover<false, 64>), grid_l, dim3(kBlock), 0, st, P);
+        HIPCHECK(hipGetLastError());
     } else if (P.n_rows) {
 #define RTW_LAUNCH(L, M) hipLaunchKernelGGL((rtw_render_f64<L, M>), grid, dim3(kBlock), lds, st, P)
         if (use_lds) {
@@ -2225,6 +2339,10 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             HIPCHECK(hipGetLastError());
         }
     }
+    hipLaunchKernelGGL(rtw_latch_check<uint32_t>, dim3(1), dim3(64), 0, st,
+                       static_cast<const uint32_t *>(P.pixels_done),
+                       static_cast<uint32_t>(static_cast<uint64_t>(P.n_rows) * P.W), s->d_err);
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(s->ev1, st));
     s->last_stream = st;
     s->pending = true;
@@ -2292,8 +2410,13 @@ void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, r
     F.counters = s->d_fcount;
     hipStream_t st = stream;
     HIPCHECK(hipSetDevice(s->device));
+    order_after_last(s, st);
     HIPCHECK(hipEventRecord(s->ev0, st));
     HIPCHECK(rtw_fast::launch(F, s->n_cu, st));
+    hipLaunchKernelGGL(rtw_latch_check<unsigned long long>, dim3(1), dim3(64), 0, st,
+                       static_cast<const unsigned long long *>(s->d_fcount + 2),
+                       static_cast<unsigned long long>(F.n_rows) * F.W, s->d_err);
+    HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(s->ev1, st));
     s->last_stream = st;
     s->pending = true;
@@ -2309,10 +2432,24 @@ void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, r
     s->last_fast = true;
 }
 
+// Latched incomplete renders since the last check (rtw_latch_check): reported
+// once, then cleared.
+void check_latch(rtw_session *s) {
+    uint32_t bad = 0;
+    HIPCHECK(hipMemcpy(&bad, s->d_err, sizeof bad, hipMemcpyDeviceToHost));
+    if (bad) {
+        HIPCHECK(hipMemset(s->d_err, 0, sizeof bad));
+        throw rtw::Error(RTW_E_HIP, std::to_string(bad) + " render(s) since the last check wrote fewer "
+                                    "pixels than the image has (incomplete image)");
+    }
+}
+
 void collect(rtw_session *s) {
     if (!s->pending) return;
     HIPCHECK(hipSetDevice(s->device));
     HIPCHECK(hipEventSynchronize(s->ev1));
+    s->pending = false;
+    check_latch(s);
     if (s->last_fast) {
         unsigned long long c[5] = {};
         HIPCHECK(hipMemcpy(c, s->d_fcount, sizeof c, hipMemcpyDeviceToHost));
@@ -2324,7 +2461,6 @@ void collect(rtw_session *s) {
         s->last.exact_wave_iterations = c[4];  // fast mode: wave-level walk iterations (RTW_FAST_DIAG builds)
         s->last.sphere_tests = c[0] * s->n_sph;
         s->last.kernel_ms = ms;
-        s->pending = false;
         if (c[2] != s->last.pixels)  // never a silently incomplete image
             throw rtw::Error(RTW_E_HIP, "fast render incomplete: " + std::to_string(c[2]) + " of " +
                                             std::to_string(s->last.pixels) + " pixels written");
@@ -2343,15 +2479,15 @@ void collect(rtw_session *s) {
     s->last.parked_pixels = c[6];
     s->last.inside_segments = c[8];
     s->last.trap_segments = c[9];
+    s->last.guard_exits = c[7];
+    s->last.leftover_pixels = c[10];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
-    s->pending = false;
     uint32_t ctl[8] = {};
     HIPCHECK(hipMemcpy(ctl, s->d_park_ctl, sizeof ctl, hipMemcpyDeviceToHost));
-    if (c[7] != 0 || ctl[4] != s->last.pixels)  // never a silently incomplete image
+    if (ctl[4] != static_cast<uint32_t>(s->last.pixels))  // never a silently incomplete image
         throw rtw::Error(RTW_E_HIP, "render incomplete: " + std::to_string(ctl[4]) + " of " +
-                                        std::to_string(s->last.pixels) + " pixels written, " +
-                                        std::to_string(c[7]) + " queue timeouts");
+                                        std::to_string(s->last.pixels) + " pixels written");
 }
 
 int default_device() {
@@ -2372,6 +2508,8 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_err, sizeof(uint32_t)));
+        HIPCHECK(hipMemset(s->d_err, 0, sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_cost_hist, kCostBuckets * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_fcursor, sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_fcount, 8 * sizeof(unsigned long long)));
@@ -2467,7 +2605,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
-    dev_free(s->d_pcost);
+    dev_free(s->d_pcost), dev_free(s->d_err);
     dev_free(s->d_fgeo), dev_free(s->d_fmat), dev_free(s->d_fkind), dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);

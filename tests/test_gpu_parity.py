@@ -333,3 +333,54 @@ def test_trapped_paths_fast_forward(monkeypatch, budget):
     if budget == "0.01":
         assert st.parked_pixels == 40 * 64
         assert st.trap_segments > 0
+
+
+@pytest.mark.parametrize("coop", ["join5", "heavy0", "default"])
+def test_no_progress_guard_and_leftover_launch(monkeypatch, coop):
+    """A zero no-progress guard (RTW_SPIN_GUARD_MS=0): waiting waves of the
+    persistent kernel leave as soon as two checks see nothing move, so claimed
+    tickets can be left behind and parked pixels published after the drain
+    waves left are finished by the follow-up launch (rtw_park_leftover). The
+    image must still be complete and bit-exact."""
+    monkeypatch.setenv("RTW_SPIN_GUARD_MS", "0")
+    monkeypatch.setenv("RTW_BUDGET_X", "0.3")
+    monkeypatch.setenv("RTW_JOIN", "5" if coop == "join5" else "0")
+    if coop == "heavy0":
+        monkeypatch.setenv("RTW_HEAVY", "0")
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
+    fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
+    ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
+    assert_same(fb, ref, st, seg)
+    assert st.parked_pixels > 0 and st.leftover_pixels <= st.parked_pixels
+    print(f"guard exits {st.guard_exits}, leftover pixels {st.leftover_pixels}")
+
+
+def test_default_guard_leaves_nothing_behind():
+    """On an exclusive device the default guard never fires: every parked pixel
+    is finished inside the persistent kernel."""
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 90, 160, 50)
+    fb, st = gpu(cam, sph, n, mt, nm, 4, SEED)
+    assert st.guard_exits == 0 and st.leftover_pixels == 0
+
+
+def test_session_renders_on_two_streams_are_serialized():
+    """Renders of one session share its device buffers: a render enqueued on a
+    second stream before the first finished must wait for it (both images exact)."""
+    torch = pytest.importorskip("torch")
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 60, 96, 50)
+    ref_a, _ = gpu(cam, sph, n, mt, nm, 3, SEED)
+    ref_b, _ = gpu(cam, sph, n, mt, nm, 2, SEED + 7)
+    sess = rtw.Session(0)
+    sess.set_scene(sph, n, mt, nm)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    a = torch.zeros((60, 96, 3), dtype=torch.float64, device="cuda:0")
+    b = torch.zeros_like(a)
+    sess.render(cam.raw, 3, SEED, a.data_ptr(), stream=s1.cuda_stream)
+    sess.render(cam.raw, 2, SEED + 7, b.data_ptr(), stream=s2.cuda_stream)
+    st = sess.stats()  # the second render's stats; the latch covers the first
+    s1.synchronize()
+    s2.synchronize()
+    assert np.array_equal(a.cpu().numpy(), ref_a)
+    assert np.array_equal(b.cpu().numpy(), ref_b)
+    assert st.pixels == 60 * 96
+    sess.close()
