@@ -370,40 +370,83 @@ struct Path {
     PathStack stk;
 };
 
+// The camera block (KParams' first 28 doubles) read at each use from the kernarg
+// segment through a pointer the compiler cannot hoist (an empty asm redefines it):
+// the s_loads land in SGPRs for the few instructions that use them, instead of 56
+// SGPRs held -- spilled to VGPR lanes and restored by v_readlane -- through the
+// whole persistent loop. Every kernel calling these helpers takes one KParams by
+// value, so it sits at kernarg offset 0.
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef const __attribute__((address_space(4))) double kdouble;
+typedef const __attribute__((address_space(4))) char kchar;
+#endif
+struct CamRef {
+#if defined(__HIP_DEVICE_COMPILE__)
+    kdouble *c;
+    __device__ __forceinline__ explicit CamRef(const KParams &) {
+        const uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+        uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+        uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+        asm volatile("" : "+s"(lo), "+s"(hi));
+        c = reinterpret_cast<kdouble *>((static_cast<uint64_t>(hi) << 32) | lo);
+    }
+#else
+    const double *c;
+    __device__ __forceinline__ explicit CamRef(const KParams &P) : c(P.p00) {}
+#endif
+    // offsets (doubles) of the KParams camera block
+    enum { kP00 = 0, kDu = 3, kDv = 6, kFrom = 9, kDdu = 12, kDdv = 15, kLatDx = 18, kLatDy = 21, kLatPos0 = 24, kDefocus = 27 };
+    __device__ __forceinline__ double operator()(int i) const { return c[i]; }
+};
+
 // get_ray, camera.rs:403: pixel_loc = (pixel00 + i*du) + j*dv
 struct PixelLoc {
     double x, y, z;
     PixelLoc() = default;
     __device__ __forceinline__ PixelLoc(const KParams &P, uint32_t px, uint32_t py) {
+        const CamRef C(P);
         const double fx = static_cast<double>(px), fy = static_cast<double>(py);
-        x = (P.p00[0] + P.du[0] * fx) + P.dv[0] * fy;
-        y = (P.p00[1] + P.du[1] * fx) + P.dv[1] * fy;
-        z = (P.p00[2] + P.du[2] * fx) + P.dv[2] * fy;
+        x = (C(C.kP00 + 0) + C(C.kDu + 0) * fx) + C(C.kDv + 0) * fy;
+        y = (C(C.kP00 + 1) + C(C.kDu + 1) * fx) + C(C.kDv + 1) * fy;
+        z = (C(C.kP00 + 2) + C(C.kDu + 2) * fx) + C(C.kDv + 2) * fy;
     }
 };
 
 // get_ray (camera.rs:400-420) with the defocus disk point (px, py) already drawn:
 // the lattice offset of sample k, the origin, the direction; starts a fresh path.
-__device__ __forceinline__ void ray_from_disk(const KParams &P, const PixelLoc &pl, uint32_t k, double px,
-                                              double py, Path &p) {
-    double offx, offy, offz;
+// offset_lattice entry k (camera.rs:422-450; k / s exactly by a multiply-high when
+// k e < 2^32, e = m s - 2^32 < s, k < s^2: s^3 <= 2^32, host: s <= 1625)
+__device__ __forceinline__ void lattice_off(const KParams &P, uint32_t k, double &offx, double &offy,
+                                            double &offz) {
+    const CamRef C(P);
     if (P.s == 0) {
-        offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
+        offx = C(C.kLatPos0 + 0), offy = C(C.kLatPos0 + 1), offz = C(C.kLatPos0 + 2);
     } else {
         const uint32_t ly = P.s_magic ? __umulhi(k, P.s_magic) : k / P.s, lx = k - ly * P.s;
         const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
-        offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
-        offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
-        offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
+        offx = (C(C.kLatPos0 + 0) + C(C.kLatDy + 0) * fly) + C(C.kLatDx + 0) * flx;
+        offy = (C(C.kLatPos0 + 1) + C(C.kLatDy + 1) * fly) + C(C.kLatDx + 1) * flx;
+        offz = (C(C.kLatPos0 + 2) + C(C.kLatDy + 2) * fly) + C(C.kLatDx + 2) * flx;
     }
-    const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
-    if (P.defocus_angle <= 0.) {
-        p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
+}
+// the ray origin: look_from, or the defocus disk point (px, py) (camera.rs:406-410, 452-456)
+__device__ __forceinline__ void ray_origin(const KParams &P, double px, double py, Path &p) {
+    const CamRef C(P);
+    if (C(C.kDefocus) <= 0.) {
+        p.ox = C(C.kFrom + 0), p.oy = C(C.kFrom + 1), p.oz = C(C.kFrom + 2);
     } else {
-        p.ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
-        p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
-        p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
+        p.ox = (C(C.kFrom + 0) + C(C.kDdu + 0) * px) + C(C.kDdv + 0) * py;
+        p.oy = (C(C.kFrom + 1) + C(C.kDdu + 1) * px) + C(C.kDdv + 1) * py;
+        p.oz = (C(C.kFrom + 2) + C(C.kDdu + 2) * px) + C(C.kDdv + 2) * py;
     }
+}
+
+__device__ __forceinline__ void ray_from_disk(const KParams &P, const PixelLoc &pl, uint32_t k, double px,
+                                              double py, Path &p) {
+    double offx, offy, offz;
+    lattice_off(P, k, offx, offy, offz);
+    const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
+    ray_origin(P, px, py, p);
     p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
     p.depth = 0;
     p.prev = -1;
@@ -415,21 +458,11 @@ __device__ __forceinline__ void ray_from_disk(const KParams &P, const PixelLoc &
 __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, uint32_t k, U128 &rng,
                                         Path &p, Stamps &stp) {
     double offx, offy, offz;
-    if (P.s == 0) {
-        offx = P.lat_pos0[0], offy = P.lat_pos0[1], offz = P.lat_pos0[2];
-    } else {
-        // k / s exactly by a multiply-high when k e < 2^32 (e = m s - 2^32 < s, k < s^2):
-        // s^3 <= 2^32 (host: s <= 1625)
-        const uint32_t ly = P.s_magic ? __umulhi(k, P.s_magic) : k / P.s, lx = k - ly * P.s;
-        const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
-        offx = (P.lat_pos0[0] + P.lat_dy[0] * fly) + P.lat_dx[0] * flx;
-        offy = (P.lat_pos0[1] + P.lat_dy[1] * fly) + P.lat_dx[1] * flx;
-        offz = (P.lat_pos0[2] + P.lat_dy[2] * fly) + P.lat_dx[2] * flx;
-    }
+    lattice_off(P, k, offx, offy, offz);
     const double sx = pl.x + offx, sy = pl.y + offy, sz = pl.z + offz;
     STAMP(8);  // 8: lattice sample position
-    if (P.defocus_angle <= 0.) {
-        p.ox = P.from[0], p.oy = P.from[1], p.oz = P.from[2];
+    if (CamRef(P)(CamRef::kDefocus) <= 0.) {
+        ray_origin(P, 0., 0., p);
     } else {
         double px, py;
         for (;;) {  // vec3.rs:270-277: strict len^2 < 1 (f32 pre-judged, as random_unit_vec)
@@ -441,9 +474,7 @@ __device__ __forceinline__ void gen_ray(const KParams &P, const PixelLoc &pl, ui
             py = -1. + 2. * rtw_num::next01_of(m1);
             if (l32 < 1.f - kRejBand || (px * px + py * py + 0. * 0.) < 1.) break;
         }
-        p.ox = (P.from[0] + P.ddu[0] * px) + P.ddv[0] * py;
-        p.oy = (P.from[1] + P.ddu[1] * px) + P.ddv[1] * py;
-        p.oz = (P.from[2] + P.ddu[2] * px) + P.ddv[2] * py;
+        ray_origin(P, px, py, p);
     }
     STAMP(9);  // 9: defocus disk sample
     p.dx = sx - p.ox, p.dy = sy - p.oy, p.dz = sz - p.oz;
