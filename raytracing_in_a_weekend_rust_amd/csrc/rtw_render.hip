@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -376,20 +377,29 @@ struct Path {
 // SGPRs held -- spilled to VGPR lanes and restored by v_readlane -- through the
 // whole persistent loop. Every kernel calling these helpers takes one KParams by
 // value, so it sits at kernarg offset 0.
+// KP(field) reads any other KParams field the same way (rarely used fields and the
+// pointers of the persistent loop: a 16-SGPR kernarg tuple restored by 16
+// v_readlane to use one pointer in it is what the compiler does otherwise).
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef const __attribute__((address_space(4))) double kdouble;
 typedef const __attribute__((address_space(4))) char kchar;
+__device__ __forceinline__ kchar *karg_base() {
+    // readfirstlane: the asm's operand must be an SGPR pair wherever the compiler
+    // keeps the segment pointer ("illegal VGPR to SGPR copy" otherwise)
+    const uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+    uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+    asm volatile("" : "+s"(lo), "+s"(hi));
+    return reinterpret_cast<kchar *>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+#define KP(f) (*reinterpret_cast<const __attribute__((address_space(4))) decltype(KParams::f) *>(karg_base() + offsetof(KParams, f)))
+#else
+#define KP(f) (P.f)
 #endif
 struct CamRef {
 #if defined(__HIP_DEVICE_COMPILE__)
     kdouble *c;
-    __device__ __forceinline__ explicit CamRef(const KParams &) {
-        const uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
-        uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-        uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-        asm volatile("" : "+s"(lo), "+s"(hi));
-        c = reinterpret_cast<kdouble *>((static_cast<uint64_t>(hi) << 32) | lo);
-    }
+    __device__ __forceinline__ explicit CamRef(const KParams &) : c(reinterpret_cast<kdouble *>(karg_base())) {}
 #else
     const double *c;
     __device__ __forceinline__ explicit CamRef(const KParams &P) : c(P.p00) {}
@@ -702,9 +712,9 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
 
 __device__ __forceinline__ void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
                                             const PixelState &ps, bool count = true) {
-    if (count && P.pixels_done) atomicAdd(P.pixels_done, 1u);
-    const double nf = static_cast<double>(P.n_off);
-    double *o = P.out + (static_cast<uint64_t>(lr) * P.W + x) * 3u;
+    if (count && KP(pixels_done)) atomicAdd(KP(pixels_done), 1u);
+    const double nf = static_cast<double>(KP(n_off));
+    double *o = KP(out) + (static_cast<uint64_t>(lr) * KP(W) + x) * 3u;
     o[0] = ps.ar / nf;
     o[1] = ps.ag / nf;
     o[2] = ps.ab / nf;
@@ -795,7 +805,8 @@ __device__ __forceinline__ bool inside_hit(const double4 *__restrict__ sph, cons
 __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restrict__ sph,
                                         const Seg32 &g, double ox, double oy, double oz, double dx,
                                         double dy, double dz, double a, double &bt, Tally &tl) {
-    const uint32_t n = P.n_sph;
+    const uint32_t n = KP(n_sph);
+    const float4 *filt = KP(filt);
     const uint32_t lane = threadIdx.x & 63u;
     int best = -1;
     for (uint32_t base = 0; base < n; base += kChunk) {
@@ -807,7 +818,7 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
             for (uint32_t q = 0; q < static_cast<uint32_t>(kChunk); q += kGroup) {
 #pragma unroll
                 for (int j = 0; j < kGroup; ++j)
-                    mask = mask + mask + static_cast<uint32_t>(g.pass(ld_filt(P.filt, base + q + j)));
+                    mask = mask + mask + static_cast<uint32_t>(g.pass(ld_filt(filt, base + q + j)));
             }
             if (cnt < static_cast<uint32_t>(kChunk)) mask &= ~((1u << (kChunk - cnt)) - 1u);
         } else {
@@ -842,16 +853,17 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
     if (sa_out) *sa_out = g.sa;  // sqrt(a): the scatter's unit(dir) divides by the same value
     bool brute = !g.fast;
     if (g.fast) {
-        for (uint32_t j = 0; j < P.n_always; ++j) {  // ground planes etc.
-            const uint32_t i = ld_const_u32(P.always, j);
-            if (g.pass(ld_filt(P.filt, i))) {
+        const uint32_t n_always = KP(n_always);
+        for (uint32_t j = 0; j < n_always; ++j) {  // ground planes etc.
+            const uint32_t i = ld_const_u32(KP(always), j);
+            if (g.pass(ld_filt(KP(filt), i))) {
                 ++tl.ntest;
                 exact_test(sph, i, ox, oy, oz, dx, dy, dz, a, best, bt);
             }
         }
         STAMP(5);  // 5: segment setup + always-spheres
         rtw_accel::WalkRay wr;
-        if (P.n_node == 0) {  // every sphere is an "always" sphere
+        if (KP(n_node) == 0) {  // every sphere is an "always" sphere
         } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
             brute = true;
         } else {
@@ -1065,13 +1077,13 @@ __device__ __forceinline__ void claim_slot(const KParams &P, uint32_t t) {
 }
 
 __device__ __forceinline__ void publish_parked(const KParams &P, const Parked &q) {
-    const uint32_t slot = atomicAdd(P.park_count, 1u);
+    const uint32_t slot = atomicAdd(KP(park_count), 1u);
     const unsigned long long *w = reinterpret_cast<const unsigned long long *>(&q);
-    gu64 *dst = (gu64 *)(P.park + slot);
+    gu64 *dst = (gu64 *)(KP(park) + slot);
 #pragma unroll
     for (int j = 0; j < 8; ++j) __hip_atomic_store(dst + j, w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store((gu32 *)(P.park_flag + slot), 1u, __ATOMIC_RELAXED,
+    __hip_atomic_store((gu32 *)(KP(park_flag) + slot), 1u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1444,15 +1456,16 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 const uint64_t m = __ballot(1);
                 const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
                 uint32_t base = 0;
-                if (rank == 0) base = atomicAdd(P.pix_cursor, static_cast<uint32_t>(__popcll(m)));
+                if (rank == 0) base = atomicAdd(KP(pix_cursor), static_cast<uint32_t>(__popcll(m)));
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
                 if (ticket < npix) {
                     // hand-out order: by descending estimated cost (P.order_map,
                     // rtw_cost_probe), so the cheapest pixels fill the drain; else
                     // rows bottom-up when P.order == 1, or row-major
-                    if (P.order_map) {
-                        pix = P.order_map[ticket];
+                    const uint32_t *order_map = KP(order_map);
+                    if (order_map) {
+                        pix = order_map[ticket];
                         lr = static_cast<uint32_t>(pix / P.W);
                         x = static_cast<uint32_t>(pix - static_cast<uint64_t>(lr) * P.W);
                     } else {
@@ -1461,7 +1474,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         lr = P.order ? P.n_rows - 1u - tr : tr;
                         pix = static_cast<uint64_t>(lr) * P.W + x;
                     }
-                    ps.rng = P.seeds[pix];
+                    ps.rng = KP(seeds)[pix];
                     ps.k = 0;
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
@@ -1548,7 +1561,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
                 if (kind != RTW_DIELECTRIC) {  // the bounce's attenuation row
                     if (ended) cr = M.a0 * 0., cg = M.a1 * 0., cb = M.a2 * 0.;  // att x black
-                    else p.stk.push(static_cast<uint32_t>(best), P.spill, stride, gid);
+                    else p.stk.push(static_cast<uint32_t>(best), KP(spill), stride, gid);
                 }
                 p.ox = hx, p.oy = hy, p.oz = hz;
                 p.dx = ndx, p.dy = ndy, p.dz = ndz;
@@ -1558,7 +1571,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             STAMP(6);  // 6: hit record + scatter without draws
             bool done = false, park = false;
             if (ended) {
-                fold(sv.shd, p, P.spill, gid, stride, cr, cg, cb);
+                fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
                 acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 done = ++ps.k >= P.n_off;
                 // park: the budget is spent, the rate runs away, or -- once the
@@ -1566,16 +1579,17 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 // estimated remaining work exceeds P.tail_segs
                 park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
                                  (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
-                if ((done || park) && P.diag) {  // a pixel's records may come from two XCDs
-                    atomicAdd(P.diag + 2 * pix, pseg);
-                    __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
+                uint32_t *diag = KP(diag);
+                if ((done || park) && diag) {  // a pixel's records may come from two XCDs
+                    atomicAdd(diag + 2 * pix, pseg);
+                    __hip_atomic_store((gu32 *)(diag + 2 * pix + 1),
                                        static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 {  // one completion-count atomic per wave (write_pixel leaves it to us)
                     const uint64_t dm = __ballot(done);
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
-                        atomicAdd(P.pixels_done, static_cast<uint32_t>(__popcll(dm)));
+                        atomicAdd(KP(pixels_done), static_cast<uint32_t>(__popcll(dm)));
                 }
             }
             STAMP(7);  // 7: fold + pixel sum + decisions
