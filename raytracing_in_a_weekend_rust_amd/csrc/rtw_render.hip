@@ -1246,15 +1246,21 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t segs, uint32_t pixels) 
     const uint32_t per = static_cast<uint32_t>((8ull * segs) / (static_cast<uint64_t>(pixels) * kProbeSamples));
     return kCostBuckets - 1u - min(per, kCostBuckets - 1u);  // 1/8 segment per sample
 }
+// Persistent: one 768-thread workgroup per CU stages the scene once and strides
+// over the pixels (a 256-thread block per 256 pixels staged ~100 KB of scene for
+// each and ran at one workgroup per CU); the walk stack lives in per-lane LDS
+// columns at P.lane_lds_off (kLds) instead of scratch memory.
+constexpr uint32_t kProbeBlock = 768;
 template <bool kLds>
-__global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
+__global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kBvh>(P, lds_sph);
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
+    uint16_t *scol = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lds_sph) + P.lane_lds_off) + threadIdx.x;
     const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
     Tally tl;
     Stamps stp;
-    if (i < npix) {
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < npix;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
         const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
         const PixelLoc pl(P, x, P.row_begin + lr * P.row_step);
         U128 rng = P.seeds[i];  // a copy: the render starts from the same child
@@ -1266,7 +1272,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_probe(const KParams P) {
                 ++segs;
                 const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
                 double bt = 0.;
-                const int best = bvh_hit(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp);
+                const int best = bvh_hit<kLds>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
                 if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
                 double cr, cg, cb;
                 shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
@@ -2276,9 +2282,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
-            const size_t lds_p = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true, P.n_nbr);
-            if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, g1, dim3(kBlock), lds_p, st, P);
-            else hipLaunchKernelGGL(rtw_cost_probe<false>, g1, dim3(kBlock), 0, st, P);
+            // probe: scene + per-lane walk stacks in LDS when they fit, one workgroup per CU
+            KParams Q = P;
+            Q.lane_lds_off = static_cast<uint32_t>((lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true, P.n_nbr) + 15) & ~size_t(15));
+            const size_t lds_p = Q.lane_lds_off + static_cast<size_t>(kProbeBlock) * rtw_accel::kScratch * sizeof(uint16_t);
+            const dim3 gp(static_cast<uint32_t>(std::min<uint64_t>(s->n_cu > 0 ? s->n_cu : 256, (npix + kProbeBlock - 1) / kProbeBlock)));
+            if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, gp, dim3(kProbeBlock), lds_p, st, Q);
+            else hipLaunchKernelGGL(rtw_cost_probe<false>, gp, dim3(kProbeBlock), 0, st, Q);
             hipLaunchKernelGGL(rtw_cost_bucket, gt, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_hot_bucket, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_scan, dim3(1), dim3(64), 0, st, P);
