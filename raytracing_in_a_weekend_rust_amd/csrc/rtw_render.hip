@@ -60,6 +60,7 @@ constexpr double kTailSegsPerSample = 768. / 529.;
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
+constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
 
 // Scene::hit strategies (one kernel instantiation each)
 constexpr int kScanF64 = 0;  // the reference's scan, f64 only
@@ -124,6 +125,8 @@ struct KParams {
     uint32_t n_cursor_waves, lane_lds_off;  // persistent kernel: byte offset of the per-lane LDS areas
     uint32_t n_nbr;             // inside-cut list entries
     uint32_t s_magic;           // ceil(2^32 / s) for k / s by a multiply-high (s <= 1625), else 0
+    uint32_t endgame;           // dry cursor and at most this many pixels unfinished: park at the
+                                // next sample boundary (0: off)
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -694,7 +697,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         bool done = shade<kTrap>(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp, &th);
         if constexpr (kTrap) {
             if (!done && (th.lam || th.tir)) {
-                const uint32_t k = trap_forward(P.trap[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
+                const uint32_t k = trap_forward(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
                 if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
             }
         }
@@ -1194,13 +1197,14 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         return best;
     };
     uint32_t s = 0, trapped = 0;
-    trace_samples<true>(P, sv, q.x, y, P.spill_b, col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    trace_samples<true>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
     if (sub == 0) tl.trap += trapped;
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
-        if (P.diag) {
-            atomicAdd(P.diag + 2 * pix, s);
-            __hip_atomic_store((gu32 *)(P.diag + 2 * pix + 1),
+        uint32_t *diag = KP(diag);
+        if (diag) {
+            atomicAdd(diag + 2 * pix, s);
+            __hip_atomic_store((gu32 *)(diag + 2 * pix + 1),
                                static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1448,6 +1452,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     if (cursor_wave) {
         bool need = true;  // lane holds no pixel
         bool dry = false;  // wave-uniform: the cursor ran dry
+        bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
         uint32_t x = 0, lr = 0, pseg = 0;
         uint64_t pix = 0;
         PixelState ps;
@@ -1496,6 +1501,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
             }
             dry = dry || __any(dry_now);  // wave-uniform
+            // endgame: once the cursor is dry and at most P.endgame pixels of the shard
+            // are unfinished (about one per drain group), every lane parks its pixel
+            // at its next sample boundary -- the last chains then run on a whole wave
+            // each (a segment every ~2 us) instead of one lane of a wave (~16 us)
+            if (dry && !endgame && P.endgame)
+                endgame = static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(ld_rlx(KP(pixels_done)))) + P.endgame >= npix;
 
             if (__all(need)) {
                 if (dry) break;
@@ -1584,6 +1595,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 // cursor is dry, so drain groups are about to be plentiful -- the
                 // estimated remaining work exceeds P.tail_segs
                 park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
+                                 (endgame && P.n_off - ps.k >= kEndgameMinSamples) ||
                                  (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
                 uint32_t *diag = KP(diag);
                 if ((done || park) && diag) {  // a pixel's records may come from two XCDs
@@ -2349,6 +2361,14 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // waves that signal the end of their cursor loop: priority waves too when they join
         P.n_cursor_waves = P.join_at != 0xffffffffu ? grid_p * wpb : grid_p * (wpb - heavy);
         P.rate_k = 16, P.rate_x = 16;
+        // endgame parking: one pixel per drain group once the cursor is dry, in shards
+        // of fewer than 2 pixels per lane of the launch (strong scaling at N >= 4: the
+        // last chains set the time; N=8 rank 86 -> 65 ms). Full images lose by it (the
+        // last pixels are cheap ones, handed out last on purpose: 152.6 -> 157.6 ms).
+        // RTW_ENDGAME: the remaining-pixel threshold, 0 = off.
+        const bool small_for_endgame = npix < 2u * static_cast<uint64_t>(grid_p) * pblock;
+        P.endgame = small_for_endgame ? grid_p * wpb * (64u / static_cast<uint32_t>(coop_g)) : 0u;
+        if (const char *e = std::getenv("RTW_ENDGAME")) P.endgame = static_cast<uint32_t>(std::atoi(e));
         P.tail_segs = small_shard ? 0xffffffffu
                                   : static_cast<uint32_t>(std::max(64., std::round(kTailSegsPerSample * P.n_off)));
         if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));

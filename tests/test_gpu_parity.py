@@ -177,6 +177,8 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0", "order0"), ("2", "0", "order1"),  # row-major / bottom-up hand-out (default: by cost)
     ("2", "0.3", "coopg16"), ("1", "0.3", "coopg16"),  # 16-lane drain groups (default: one wave)
     ("2", "0.3", "join5"), ("2", "1.5", "join50"),  # priority waves join the cursor (RTW_JOIN %)
+    ("2", "0", "endgame"), ("2", "0.3", "endgame"),  # dry cursor: park everything (RTW_ENDGAME)
+    ("2", "0", "endgame_coopg16"),
 ]
 
 
@@ -194,6 +196,10 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_ORDER", {"order0": "0", "order1": "1"}.get(coop, "2"))
     monkeypatch.setenv("RTW_COOPG", "16" if coop == "coopg16" else "64")
     monkeypatch.setenv("RTW_JOIN", {"join5": "5", "join50": "50"}.get(coop, "0"))
+    endgame = coop.startswith("endgame")
+    monkeypatch.setenv("RTW_ENDGAME", "100000000" if endgame else "0")
+    if coop == "endgame_coopg16":
+        monkeypatch.setenv("RTW_COOPG", "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
     fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
     ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
@@ -201,8 +207,10 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     assert st.accel == int(accel)
     if budget == "0.01":
         assert st.parked_pixels == 45 * 80
-    if budget == "0" and coop != "rate1":
+    if budget == "0" and coop != "rate1" and not endgame:
         assert st.parked_pixels == 0
+    if endgame:
+        assert st.parked_pixels > 0
     if coop == "rate1":
         assert st.parked_pixels > 45 * 80 // 2
     if accel == "2" and budget == "0":
