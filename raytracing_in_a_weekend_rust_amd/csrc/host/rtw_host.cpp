@@ -312,21 +312,89 @@ static inline uint64_t sat_u64(double v) {
     if (v >= 18446744073709551616.0) return UINT64_MAX;
     return static_cast<uint64_t>(v);
 }
+// gamma_correct + quantise (color.rs:241-247): (c.powf(1/2.2) * 255.0) as u64.
+static inline uint64_t quantise_pow(double c) { return sat_u64(std::pow(c, 1. / 2.2) * 255.); }
+static inline uint64_t bits_of(double x) {
+    uint64_t u;
+    std::memcpy(&u, &x, 8);
+    return u;
+}
+// The same value without a pow call for c in (0, 1): c's value is the number of
+// thresholds T_1..T_255 it reaches, T_k = the smallest double with quantise_pow >= k
+// (found once by bisection over the bit patterns of [0, 1], with the library pow
+// itself). pow is accurate to < 1 ulp, and near T_k the true c^(1/2.2) x 255 moves
+// by ~0.45 ulp per ulp of c, so any wobble of the rounded result around k stays
+// within a few ulps of T_k: inputs within kNear ulps of a threshold, c >= 1 and
+// c <= 0 / NaN take quantise_pow itself. Equal to quantise_pow for every input
+// (tests/test_host_abi.py checks millions of them and every threshold's neighbourhood).
+struct GammaTable {
+    static constexpr uint64_t kNear = 64;
+    uint64_t t[257];  // t[0] = 0, t[k] = bits of T_k, t[256] = bits of 1.0
+    GammaTable() {
+        t[0] = 0;
+        for (uint32_t k = 1; k <= 255; ++k) {
+            uint64_t lo = t[k - 1], hi = bits_of(1.0);  // quantise_pow(lo) < k <= quantise_pow(hi)
+            while (hi - lo > 1) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                double m;
+                std::memcpy(&m, &mid, 8);
+                if (quantise_pow(m) >= k) hi = mid;
+                else lo = mid;
+            }
+            t[k] = hi;
+        }
+        t[256] = bits_of(1.0);
+    }
+    uint64_t operator()(double c) const {
+        if (!(c > 0.) || !(c < 1.)) return quantise_pow(c);
+        const uint64_t b = bits_of(c);
+        uint32_t k = 0;  // largest k with t[k] <= b (t[0] = 0 <= b)
+        for (uint32_t step = 128; step; step >>= 1)
+            if (k + step <= 255 && t[k + step] <= b) k += step;
+        if (b - t[k] < kNear || (k < 255 && t[k + 1] - b <= kNear)) return quantise_pow(c);
+        return k;
+    }
+};
+static const GammaTable &gamma_table() {
+    static const GammaTable g;
+    return g;
+}
+uint64_t quantise_channel(double c, bool direct) { return direct ? quantise_pow(c) : gamma_table()(c); }
+
+// Decimal text of 0..255 (the values of a [0, 1] channel): length + digits.
+struct SmallDigits {
+    char d[256][4];
+    uint8_t n[256];
+    SmallDigits() {
+        for (uint32_t v = 0; v < 256; ++v) n[v] = static_cast<uint8_t>(std::snprintf(d[v], 4, "%u", v));
+    }
+};
 static void format_rows(const double *rgb, uint32_t w, uint32_t y0, uint32_t y1, std::string &s) {
-    char tmp[24];
+    static const SmallDigits sd;
+    const GammaTable &gt = gamma_table();
+    std::vector<char> line(static_cast<size_t>(w) * 3 * 21 + 1);  // 20 digits + separator each
     for (uint32_t y = y0; y < y1; ++y) {
         const double *row = rgb + static_cast<size_t>(y) * w * 3;
+        char *o = line.data();
         for (uint64_t i = 0; i < 3ull * w; ++i) {
-            const double g = std::pow(row[i], 1. / 2.2);  // gamma_correct, color.rs:241-247
-            uint64_t v = sat_u64(g * 255.);
-            char *e = tmp + sizeof tmp, *b = e;  // decimal digits, right to left
-            do {
-                *--b = static_cast<char>('0' + v % 10u);
-                v /= 10u;
-            } while (v);
-            s.append(b, static_cast<size_t>(e - b));
-            s.push_back(i + 1 == 3ull * w ? '\n' : ' ');
+            uint64_t v = gt(row[i]);  // gamma_correct, color.rs:241-247
+            if (v < 256) {
+                std::memcpy(o, sd.d[v], 4);  // 4 bytes copied, n[v] kept
+                o += sd.n[v];
+            } else {
+                char tmp[24];
+                char *e = tmp + sizeof tmp, *b = e;  // decimal digits, right to left
+                do {
+                    *--b = static_cast<char>('0' + v % 10u);
+                    v /= 10u;
+                } while (v);
+                std::memcpy(o, b, static_cast<size_t>(e - b));
+                o += e - b;
+            }
+            *o++ = ' ';
         }
+        if (o != line.data()) o[-1] = '\n';  // color.rs:226-233: one text line per image row
+        s.append(line.data(), static_cast<size_t>(o - line.data()));
     }
 }
 // color.rs:196-239. Rows are formatted in parallel chunks (the reference's

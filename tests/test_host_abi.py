@@ -140,6 +140,42 @@ def test_ppm_writer_edge_values_and_parallel_rows():
     assert rtw.format_ppm(fb) == orc.format_ppm(fb)
 
 
+def _gamma_thresholds():
+    """T_k = the smallest double c with int(c ** (1/2.2) * 255) >= k (k = 1..255), by
+    bisection over bit patterns with the C library's pow (math.pow), as in rtw_host.cpp."""
+    def q(b):
+        return int(math.pow(float(np.array([b], dtype=np.uint64).view(np.float64)[0]), 1. / 2.2) * 255.)
+    one = int(np.array([1.0]).view(np.uint64)[0])
+    t, lo = [], 0
+    for k in range(1, 256):
+        hi = one
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            if q(mid) >= k:
+                hi = mid
+            else:
+                lo = mid
+        t.append(hi)
+    return np.array(t, dtype=np.uint64)
+
+
+def test_ppm_gamma_table_equals_pow_everywhere():
+    """The PPM writer's threshold table (rtw_host.cpp GammaTable) gives exactly
+    (c.powf(1/2.2) * 255.0) as u64 (color.rs:241-247): every threshold's +-300-ulp
+    neighbourhood, 3M random values in [0, 1], and [0, 1.2] with specials, against
+    the oracle's formatter (a pow call per channel)."""
+    t = _gamma_thresholds()
+    offs = np.arange(-300, 301, dtype=np.int64)
+    near = (t[:, None].astype(np.int64) + offs[None, :]).ravel().astype(np.uint64).view(np.float64)
+    rng = np.random.default_rng(11)
+    vals = np.concatenate([near, rng.random(3_000_000), rng.random(200_000) ** 8, rng.random(100_000) * 1.2,
+                           [0.0, -0.0, 1.0, np.nextafter(1.0, 0.0), 5e-324, -1e-300, math.nan, math.inf]])
+    w = 1000
+    vals = np.concatenate([vals, np.zeros((-len(vals)) % (3 * w))])
+    fb = vals.reshape(-1, w, 3)
+    assert rtw.format_ppm(fb) == orc.format_ppm(fb)
+
+
 def test_ppm_writer_bright_image_outgrows_first_buffer():
     # > 4 bytes per channel: the Python mirror's first buffer is too small and it
     # retries at the size the ABI reports
