@@ -411,6 +411,13 @@ struct CamRef {
     enum { kP00 = 0, kDu = 3, kDv = 6, kFrom = 9, kDdu = 12, kDdv = 15, kLatDx = 18, kLatDy = 21, kLatPos0 = 24, kDefocus = 27 };
     __device__ __forceinline__ double operator()(int i) const { return c[i]; }
 };
+static_assert(offsetof(KParams, p00) == 8 * CamRef::kP00 && offsetof(KParams, du) == 8 * CamRef::kDu &&
+                  offsetof(KParams, dv) == 8 * CamRef::kDv && offsetof(KParams, from) == 8 * CamRef::kFrom &&
+                  offsetof(KParams, ddu) == 8 * CamRef::kDdu && offsetof(KParams, ddv) == 8 * CamRef::kDdv &&
+                  offsetof(KParams, lat_dx) == 8 * CamRef::kLatDx && offsetof(KParams, lat_dy) == 8 * CamRef::kLatDy &&
+                  offsetof(KParams, lat_pos0) == 8 * CamRef::kLatPos0 &&
+                  offsetof(KParams, defocus_angle) == 8 * CamRef::kDefocus,
+              "CamRef offsets follow the KParams camera block");
 
 // get_ray, camera.rs:403: pixel_loc = (pixel00 + i*du) + j*dv
 struct PixelLoc {
