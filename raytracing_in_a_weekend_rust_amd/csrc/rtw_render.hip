@@ -52,7 +52,10 @@ constexpr int kChunk = 32;                // spheres per candidate mask (one bit
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
 constexpr int kCounters = 12;
-constexpr double kBudgetX = 10.0;       // park a pixel past this many segments x samples per pixel
+// park a pixel past this many segments x samples per pixel (10 -> 14 in round 2: the
+// faster kernel leaves fewer pixels worth a whole drain wave; 12-17 all 151.4-151.5 ms
+// vs 153.2 ms at 10, interleaved A/B, profiles/r02_misc/knobs_budget.log)
+constexpr double kBudgetX = 14.0;
 // dry-cursor parking: estimated segments left (RTW_TAIL), per lattice sample of the
 // pixel: 768 at 529 spp (tuned there); 145 at 100 spp and 2940 at 2025 spp measured
 // better than a fixed 768 (38.1 -> 36.1 ms; 1026 -> 864 ms per rank of 8 at 4096x2304)
