@@ -654,10 +654,21 @@ __device__ __forceinline__ uint32_t trap_forward(const double4 T, uint32_t rem, 
 
 // att0 * (att1 * (... * leaf)) -- right-to-left, as the recursion associates
 // (camera.rs:389); then the sample's colour is added to the pixel sum.
+// The spilled levels (deepest, rare) first; then the register levels, whose row
+// index is picked branch-free (a select of r0 / r1 and a shift), so the wave runs
+// one short loop body per level instead of a three-way branch.
 __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, const uint16_t *spill,
                                      uint64_t col, uint64_t stride, double &lr, double &lg, double &lb) {
-    for (uint32_t j = p.stk.n; j-- > 0;) {
-        const ShadeRec &A = shd[p.stk.at(j, spill, stride, col)];
+    const uint32_t n = p.stk.n;
+    for (uint32_t j = n; j-- > kRegSlots;) {
+        const ShadeRec &A = shd[spill[static_cast<uint64_t>(j - kRegSlots) * stride + col]];
+        lr = A.a0 * lr;
+        lg = A.a1 * lg;
+        lb = A.a2 * lb;
+    }
+    for (uint32_t j = n < kRegSlots ? n : kRegSlots; j-- > 0;) {
+        const uint64_t w = j < 4u ? p.stk.r0 : p.stk.r1;
+        const ShadeRec &A = shd[static_cast<uint32_t>(w >> (16u * (j & 3u))) & 0xffffu];
         lr = A.a0 * lr;
         lg = A.a1 * lg;
         lb = A.a2 * lb;
