@@ -1637,34 +1637,37 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             // judged in f32 first and rebuilt exactly only near the boundary
             const bool want_u = kind <= RTW_METAL;  // Lambertian or Metal
             const bool want_disk = ended && !done && !park && !(P.defocus_angle <= 0.);
+            // The loop keeps only the accepted raw draws; their f64 coordinates are formed
+            // once after it (inside it, only the rare candidates within 2^-17 of the
+            // boundary need them, for the exact test).
             uint32_t phase = want_u ? 1u : want_disk ? 2u : 0u;
-            double ux = 0., uy = 0., uz = 0., ul2 = 1., dpx = 0., dpy = 0.;
+            uint32_t um0 = 0, um1 = 0, um2 = 0, dm0 = 0, dm1 = 0;  // accepted draws (sphere, disk)
             while (phase) {
                 const uint32_t m0 = xs_next_m(ps.rng), m1 = xs_next_m(ps.rng);
                 uint32_t m2 = 0;
                 if (phase == 1u) m2 = xs_next_m(ps.rng);
                 const float x32 = coord32(m0), y32 = coord32(m1), z32 = phase == 1u ? coord32(m2) : 0.f;
                 const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
-                if (l32 > 1.f + kRejBand) continue;  // surely rejected
-                if (phase == 1u) {
-                    const double x = coord64(m0), y = coord64(m1), z = coord64(m2);
-                    const double l2 = x * x + y * y + z * z;
-                    if (l32 < 1.f - kRejBand || l2 <= 1.) {
-                        ux = x, uy = y, uz = z, ul2 = l2;
-                        phase = want_disk ? 2u : 0u;
+                bool ok = l32 < 1.f - kRejBand;  // surely accepted
+                if (!ok && !(l32 > 1.f + kRejBand)) {  // near the boundary: the exact test
+                    const double x = coord64(m0), y = coord64(m1);
+                    if (phase == 1u) {
+                        const double z = coord64(m2);
+                        ok = x * x + y * y + z * z <= 1.;          // vec3.rs:219-226
+                    } else {
+                        ok = (x * x + y * y + 0. * 0.) < 1.;      // vec3.rs:270-277
                     }
-                } else {
-                    const double px = -1. + 2. * rtw_num::next01_of(m0);
-                    const double py = -1. + 2. * rtw_num::next01_of(m1);
-                    if (l32 < 1.f - kRejBand || (px * px + py * py + 0. * 0.) < 1.) {
-                        dpx = px, dpy = py;
-                        phase = 0u;
-                    }
+                }
+                if (ok) {
+                    if (phase == 1u) um0 = m0, um1 = m1, um2 = m2, phase = want_disk ? 2u : 0u;
+                    else dm0 = m0, dm1 = m1, phase = 0u;
                 }
             }
             STAMP(9);  // 9: the draws
+            double ux, uy, uz;
             if (want_u && !ended) {  // materials.rs:22-37 / 52-63 with u = unit(the point)
-                const double l = __builtin_sqrt(ul2);
+                ux = coord64(um0), uy = coord64(um1), uz = coord64(um2);
+                const double l = __builtin_sqrt(ux * ux + uy * uy + uz * uz);
                 ux = ux / l, uy = uy / l, uz = uz / l;
                 double ndx = p.dx + ux * fz, ndy = p.dy + uy * fz, ndz = p.dz + uz * fz;
                 // near_zero without abs (vec3.rs:246-250): Lambertian falls back to n
@@ -1685,7 +1688,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     publish_parked(P, q);
                     ++tl.parked;
                     need = true;
-                } else {
+                } else {  // the next sample's defocus disk point (camera.rs:452-456)
+                    const double dpx = -1. + 2. * rtw_num::next01_of(dm0), dpy = -1. + 2. * rtw_num::next01_of(dm1);
                     ray_from_disk(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, dpx, dpy, p);
                 }
             }
