@@ -192,28 +192,31 @@ RTW_HD bool slab_hit(float nx, float ny, float nz, float fx, float fy, float fz,
     return fmaxf(tn, r.tmin) <= fminf(tf, U);
 }
 
-// The pass-1 filter on leaf k; a kept sphere joins the candidate list (false on
-// overflow) and, if it is a sure hit (disc beyond the filter's inflation + error,
-// far root clearly past tmin), its far root bounds the closest hit: U shrinks.
+// The pass-1 filter on leaf k; a kept sphere joins the candidate list (an
+// overflow is recorded in the scratch, the walk stops after the node) and, if it
+// is a sure hit (disc beyond the filter's inflation + error, far root clearly past
+// tmin), its far root bounds the closest hit: U shrinks. Both loads are issued
+// together and the sure-hit bound is a select, not a branch: the wave runs this
+// body once per leaf of its busiest lane, so every branch in it is paid by all.
 template <typename F4, typename Scratch>
-RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &r, float &U,
+RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &r, float &U,
                       Scratch &ws) {
     const F4 S = leaves[2 * k];
+    const float d2 = leaves[2 * k + 1].x;
     const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
-    if (disc < r.negG) return true;
-    if (!ws.add_cand(k)) return false;
-    const float d2 = leaves[2 * k + 1].x;
-    if (disc > d2 - 2.f * r.negG) {
-        const float sd = sqrt32(disc);
-        const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
-        const float sfar = sd - hb;
-        const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
-        if (slo - slack > r.tmin * 1.001f) U = fminf(U, sfar + slack);
-    }
-    return true;
+    if (disc < r.negG) return;
+    ws.add_cand(k);
+    // sure hit iff disc > d2 - 2 negG (> 0: sd is then a real root; otherwise
+    // sd and slo are unused)
+    const float sd = sqrt32(disc);
+    const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
+    const float sfar = sd - hb;
+    const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
+    const bool sure = disc > d2 - 2.f * r.negG && slo - slack > r.tmin * 1.001f;
+    U = sure ? fminf(U, sfar + slack) : U;
 }
 
 // Walk scratch: the traversal stack of 16-bit node ids (LIFO) and the candidate
@@ -223,25 +226,30 @@ RTW_HD bool leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
 // puts every child slot far to near without branching, so up to 4 slots above
 // the kept entries are written. Invariant: kept + 4 + candidates <= kScratch
 // (else overflow: the caller brute-forces), at most kMaxCand candidates.
+// add_cand never exits the walk: a candidate that does not fit sets `bad` (its
+// store goes to the unclaimed next candidate slot, always inside the column), and
+// overflow() ends the walk after the node.
 constexpr uint32_t kScratch = 24;
 // ArrayScratch (host, accel_check): a plain array.
 struct ArrayScratch {
     uint16_t e[kScratch] = {};
     uint32_t sp = 0, nc = 0;
+    uint32_t bad = 0;  // a u32, not a bool: no lane-mask merges in the leaf loop
     RTW_HD void put(uint32_t id, uint32_t h) {
         e[sp] = static_cast<uint16_t>(id);
         sp += h;
     }
-    RTW_HD bool overflow() const { return sp + 4u + nc > kScratch; }
+    RTW_HD bool overflow() const { return bad != 0u || sp + 4u + nc > kScratch; }
     RTW_HD bool pop(uint32_t &next) {
         if (sp == 0) return false;
         next = e[--sp];
         return true;
     }
-    RTW_HD bool add_cand(uint32_t k) {
-        if (nc >= kMaxCand || sp + 5u + nc > kScratch) return false;
-        e[kScratch - 1u - nc++] = static_cast<uint16_t>(k);
-        return true;
+    RTW_HD void add_cand(uint32_t k) {
+        const bool ok = nc < kMaxCand && sp + 5u + nc <= kScratch;
+        e[kScratch - 1u - nc] = static_cast<uint16_t>(k);
+        nc += ok ? 1u : 0u;
+        bad |= ok ? 0u : 1u;
     }
     RTW_HD uint32_t cand_at(uint32_t j) const { return e[kScratch - 1u - j]; }
 };
@@ -252,6 +260,7 @@ struct ArrayScratch {
 struct LdsScratch {
     uint16_t *base, *top, *cand, *lim;
     uint32_t stride, nc = 0;
+    uint32_t bad = 0;  // a u32, not a bool: no lane-mask merges in the leaf loop
     __device__ LdsScratch(uint16_t *c, uint32_t s)
         : base(c), top(c), cand(c + (kScratch - 1u) * s), lim(c + (kScratch - 4u) * s), stride(s) {}
     __device__ void put(uint32_t id, uint32_t h) {
@@ -259,18 +268,21 @@ struct LdsScratch {
         // h in {0, 1}: one v_mad_u32_u24 on the byte address
         top = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(top) + __umul24(h, 2u * stride));
     }
-    __device__ bool overflow() const { return top > lim; }
+    __device__ bool overflow() const { return bad != 0u || top > lim; }
     __device__ bool pop(uint32_t &next) {
         if (top == base) return false;
         top -= stride;
         next = *top;
         return true;
     }
-    __device__ bool add_cand(uint32_t k) {
-        if (nc >= kMaxCand || top >= lim) return false;
+    __device__ void add_cand(uint32_t k) {
+        const bool ok = nc < kMaxCand && top < lim;
         *cand = static_cast<uint16_t>(k);
-        cand -= stride, lim -= stride, ++nc;
-        return true;
+        const uint32_t step = ok ? 2u * stride : 0u;  // bytes
+        cand = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(cand) - step);
+        lim = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lim) - step);
+        nc += ok ? 1u : 0u;
+        bad |= ok ? 0u : 1u;
     }
     __device__ uint32_t cand_at(uint32_t j) const { return base[(kScratch - 1u - j) * stride]; }
 };
@@ -319,16 +331,15 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         // leaf children first: they may tighten U for the inner children
         uint32_t lmask = hit & (masks >> 4);
         const uint32_t inner = hit & ~lmask & 15u;
+        const uint64_t refs = (static_cast<uint64_t>(r23) << 32) | r01;
         while (lmask) {
             const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
             lmask &= lmask - 1u;
-            const uint32_t k = ((j & 2u ? r23 : r01) >> (16u * (j & 1u))) & 0xffffu;
-            if (!leaf_test(leaves, k, r, U, stk)) return false;
+            leaf_test(leaves, static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, r, U, stk);
         }
         // hit inner children onto the stack far to near (branch-free puts), then
         // continue with the top = the nearest
         const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
-        const uint64_t refs = (static_cast<uint64_t>(r23) << 32) | r01;
         for (int t = 3; t >= 0; --t) {
             const uint32_t j = (ord >> (2 * t)) & 3u;
 #if defined(__HIP_DEVICE_COMPILE__)
