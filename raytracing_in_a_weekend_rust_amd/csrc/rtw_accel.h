@@ -227,8 +227,9 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
 // the kept entries are written. Invariant: kept + 4 + candidates <= kScratch
 // (else overflow: the caller brute-forces), at most kMaxCand candidates.
 // add_cand never exits the walk: a candidate that does not fit sets `bad` (its
-// store goes to the unclaimed next candidate slot, always inside the column), and
-// overflow() ends the walk after the node.
+// store goes to the unclaimed next candidate slot, always inside the column).
+// next() ends the node: it records a stack overflow in `bad` and pops the next
+// node unless the stack is empty or the walk has failed -- the walk's one exit.
 constexpr uint32_t kScratch = 24;
 // ArrayScratch (host, accel_check): a plain array.
 struct ArrayScratch {
@@ -239,10 +240,10 @@ struct ArrayScratch {
         e[sp] = static_cast<uint16_t>(id);
         sp += h;
     }
-    RTW_HD bool overflow() const { return bad != 0u || sp + 4u + nc > kScratch; }
-    RTW_HD bool pop(uint32_t &next) {
-        if (sp == 0) return false;
-        next = e[--sp];
+    RTW_HD bool next(uint32_t &id) {
+        bad |= sp + 4u + nc > kScratch ? 1u : 0u;
+        if (bad != 0u || sp == 0) return false;
+        id = e[--sp];
         return true;
     }
     RTW_HD void add_cand(uint32_t k) {
@@ -268,11 +269,11 @@ struct LdsScratch {
         // h in {0, 1}: one v_mad_u32_u24 on the byte address
         top = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(top) + __umul24(h, 2u * stride));
     }
-    __device__ bool overflow() const { return bad != 0u || top > lim; }
-    __device__ bool pop(uint32_t &next) {
-        if (top == base) return false;
+    __device__ bool next(uint32_t &id) {
+        bad |= top > lim ? 1u : 0u;
+        if (bad != 0u || top == base) return false;
         top -= stride;
-        next = *top;
+        id = *top;
         return true;
     }
     __device__ void add_cand(uint32_t k) {
@@ -348,10 +349,9 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
             stk.put(static_cast<uint32_t>(refs >> (16u * j)), (inner >> j) & 1u);
 #endif
         }
-        if (stk.overflow()) return false;
-        if (!stk.pop(cur)) break;
+        if (!stk.next(cur)) break;
     }
-    return true;
+    return stk.bad == 0u;
 }
 
 // (t, i) beats (bt, best) under the scan's first-minimum rule.

@@ -354,13 +354,16 @@ struct SceneView {
 };
 // inside-cut list entries (u16) in float4 units
 __host__ __device__ constexpr uint32_t nbr_f4(uint32_t n_nbr) { return (n_nbr + 7u) / 8u; }
-// LDS layout: [n] double4 sph | [n] ShadeRec | (BVH) [9 n_node] + [2 n_leaf] float4 +
-// inside-cut lists (padded to float4)
+// BVH nodes in float4 units, padded to 32 B (the double4 records after them)
+__host__ __device__ constexpr uint32_t node_area_f4(uint32_t n_node) { return (rtw_accel::kNodeF4 * n_node + 1u) & ~1u; }
+// LDS layout: (BVH) [node_area_f4] nodes + [2 n_leaf] leaves (float4) first -- the
+// walk's node addresses are then id * 144 with no base register -- then [n] double4
+// sph | [n] ShadeRec | (BVH) inside-cut lists (padded to float4)
 __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh,
                                                 uint32_t n_nbr = 0) {
     return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
-           (bvh ? (rtw_accel::kNodeF4 * static_cast<size_t>(n_node) + 2 * static_cast<size_t>(n_leaf) +
-                   nbr_f4(n_nbr)) * sizeof(float4)
+           (bvh ? (static_cast<size_t>(node_area_f4(n_node)) + 2 * static_cast<size_t>(n_leaf) + nbr_f4(n_nbr)) *
+                      sizeof(float4)
                 : 0);
 }
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
@@ -954,23 +957,27 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
     SceneView v{P.sph, P.shade, P.nodes, P.leaves, P.nbr};
     if (kLds) {
         const uint32_t n = P.n_sph;
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) lds[i] = P.sph[i];
-        ShadeRec *ls = reinterpret_cast<ShadeRec *>(lds + n);
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
-        float4 *lf = reinterpret_cast<float4 *>(ls + n);
-        if (kMode == kBvh) {
-            const uint32_t nn = rtw_accel::kNodeF4 * P.n_node, nl = 2u * P.n_leaf;
+        double4 *ld = lds;
+        if (kMode == kBvh) {  // nodes at LDS offset 0, then the leaves
+            float4 *lf = reinterpret_cast<float4 *>(lds);
+            const uint32_t nn = rtw_accel::kNodeF4 * P.n_node, na = node_area_f4(P.n_node), nl = 2u * P.n_leaf;
             for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) lf[i] = P.nodes[i];
-            for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) lf[nn + i] = P.leaves[i];
-            uint16_t *lnb = reinterpret_cast<uint16_t *>(lf + nn + nl);
+            for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) lf[na + i] = P.leaves[i];
+            v.nodes = lf;
+            v.leaves = lf + na;
+            ld = reinterpret_cast<double4 *>(lf + na + nl);
+        }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ld[i] = P.sph[i];
+        ShadeRec *ls = reinterpret_cast<ShadeRec *>(ld + n);
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
+        if (kMode == kBvh) {
+            uint16_t *lnb = reinterpret_cast<uint16_t *>(ls + n);
             for (uint32_t i = threadIdx.x; i < P.n_nbr; i += blockDim.x) lnb[i] = P.nbr[i];
             v.nbr = lnb;
         }
         __syncthreads();
-        v.sph = lds;
+        v.sph = ld;
         v.shd = ls;
-        v.nodes = lf;
-        v.leaves = lf + rtw_accel::kNodeF4 * P.n_node;
     }
     return v;
 }
@@ -1381,9 +1388,10 @@ template <bool kLds, int kMode, uint32_t kThreads, uint32_t kCoopG = 16>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
-    // pass-1 records after the scene view: after the leaves (BVH) or the shading records
-    float4 *filt_lds = reinterpret_cast<float4 *>(reinterpret_cast<ShadeRec *>(lds_sph + P.n_sph) + P.n_sph);
-    if (kMode == kBvh) filt_lds += rtw_accel::kNodeF4 * P.n_node + 2u * P.n_leaf + nbr_f4(P.n_nbr);
+    // pass-1 records after the scene view: after the inside-cut lists (BVH) or the
+    // shading records
+    float4 *filt_lds = reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph);
+    if (kMode == kBvh) filt_lds += nbr_f4(P.n_nbr);
     const float4 *filt = stage_filt<kLds>(P, filt_lds);
     // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
     // read and written once per sample) and the BVH walk scratch (kScratch u16

@@ -30,3 +30,7 @@ print(f"s={s} kernel_ms={st.kernel_ms:.1f} cursor waves={len(rows)} wave iterati
 for k, nme in enumerate(names):
     print(f"  {nme:17s} {tot[k] / tot.sum() * 100:6.2f}%  {tot[k] / wi:8.0f} cyc/wave-iter")
 print(f"  total {tot.sum() / wi:.0f} cycles per wave-iteration (sections are max over lanes: an upper bound)")
+cnt = rows[:, 10:14].sum(axis=0).astype(np.float64)
+if cnt.any():
+    print(f"draws loop: {cnt[0] / wi:.2f} wave trips per wave-iteration; per wave-iteration lanes needing a unit "
+          f"vector {cnt[1] / wi:.1f}, drawn by the speculation {cnt[2] / wi:.1f}, speculations discarded {cnt[3] / wi:.1f}")
