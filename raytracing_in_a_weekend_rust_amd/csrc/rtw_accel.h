@@ -230,7 +230,7 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
 // store goes to the unclaimed next candidate slot, always inside the column).
 // next() ends the node: it records a stack overflow in `bad` and pops the next
 // node unless the stack is empty or the walk has failed -- the walk's one exit.
-constexpr uint32_t kScratch = 24;
+constexpr uint32_t kScratch = 16;
 // ArrayScratch (host, accel_check): a plain array.
 struct ArrayScratch {
     uint16_t e[kScratch] = {};

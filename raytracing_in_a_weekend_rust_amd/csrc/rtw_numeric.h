@@ -42,4 +42,50 @@ RTW_NHD double next01_of(uint32_t m) {
     return s;
 }
 
+// ---- f64 divisions by one divisor sharing its reciprocal (device) ----------
+// The compiler's IEEE f64 division x / d is: v_div_scale of d and of x, v_rcp_f64
+// of the scaled d, two Newton steps r <- r + r (1 - d r), q0 = x r, the correction
+// q = q0 + r (x - d q0) (v_div_fmas) and v_div_fixup. With |x| and |d| in
+// [2^-256, 2^256] both scale steps are the identity (v_div_scale scales only for
+// exponent gaps >= 768, denormal or near-overflow operands, or a numerator exponent
+// <= 53) and so is the fixup (finite nonzero quotient, sign already right). Then
+// divisions by the same d can share the reciprocal and its Newton steps: the same
+// operations in the same order, the same bits. Outside the range: plain division.
+// (Biased exponent e in [1023 - 256, 1023 + 256]: (e - 767) < 513 unsigned.)
+RTW_NHD uint32_t div_exp_off(double v) {
+    uint64_t u;
+    memcpy(&u, &v, 8);
+    return (static_cast<uint32_t>(u >> 52) & 0x7ffu) - 767u;
+}
+RTW_NHD bool div_range(double v) { return div_exp_off(v) < 513u; }
+// d's reciprocal after the two Newton steps, or 0 when d is out of range
+RTW_NHD double div_rcp(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (!div_range(d)) return 0.;
+    const double r0 = __builtin_amdgcn_rcp(d);
+    const double r1 = __builtin_fma(r0, __builtin_fma(-d, r0, 1.), r0);
+    return __builtin_fma(r1, __builtin_fma(-d, r1, 1.), r1);
+#else
+    (void)d;
+    return 0.;
+#endif
+}
+// x / d given r = div_rcp(d) != 0 and div_range(x)
+RTW_NHD double div_q(double x, double d, double r) {
+    const double q0 = x * r;
+    return __builtin_fma(__builtin_fma(-d, q0, x), r, q0);
+}
+// (x, y, z) / d, one range test for the three
+RTW_NHD void div3(double &x, double &y, double &z, double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double r = div_rcp(d);
+    const uint32_t m = div_exp_off(x) > div_exp_off(y) ? div_exp_off(x) : div_exp_off(y);
+    if (r != 0. && (m > div_exp_off(z) ? m : div_exp_off(z)) < 513u) {
+        x = div_q(x, d, r), y = div_q(y, d, r), z = div_q(z, d, r);
+        return;
+    }
+#endif
+    x = x / d, y = y / d, z = z / d;
+}
+
 }  // namespace rtw_num

@@ -265,9 +265,8 @@ __device__ __forceinline__ void random_unit_vec(U128 &rng, double &ux, double &u
         if (l32 < 1.f - kRejBand || l2 <= 1.) break;  // surely / exactly accepted
     }
     const double l = __builtin_sqrt(l2);
-    ux = x / l;
-    uy = y / l;
-    uz = z / l;
+    rtw_num::div3(x, y, z, l);  // x / l, y / l, z / l (one shared reciprocal, same bits)
+    ux = x, uy = y, uz = z;
 }
 
 // Material rows of the current path's non-dielectric bounces (dielectric
@@ -367,9 +366,10 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
                 : 0);
 }
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
-// sum (3 x f64 columns) and the BVH walk scratch (kScratch x u16 columns).
+// sum (3 x f64 columns), the BVH walk scratch (kScratch x u16 columns) and the
+// speculative draws' RNG state (one 16 B column).
 __host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
-    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t));
+    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t) + 16);
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -534,8 +534,8 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     const uint32_t kind = best >= 0 ? shd[best].kind : 3u;  // 3: the sky
     double vx = 0., vy = 0., vz = 0.;
     if (kind != RTW_LAMBERTIAN) {
-        const double l = __builtin_sqrt(a);
-        vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+        vx = p.dx, vy = p.dy, vz = p.dz;
+        rtw_num::div3(vx, vy, vz, __builtin_sqrt(a));  // unit(dir): / l, one shared reciprocal
     }
     if (best < 0) {
         const double t = 0.5 * (vy + 1.0);
@@ -550,7 +550,8 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     const ShadeRec M = shd[best];
     const double r = M.r;
     const double px = p.dx * bt + p.ox, py = p.dy * bt + p.oy, pz = p.dz * bt + p.oz;
-    double nx = (px - S.x) / r, ny = (py - S.y) / r, nz = (pz - S.z) / r;
+    double nx = px - S.x, ny = py - S.y, nz = pz - S.z;
+    rtw_num::div3(nx, ny, nz, r);  // (p - c) / r
     const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
     if constexpr (kTrap) th->h0x = nx, th->h0y = ny, th->h0z = nz;
     if (!front) nx = -nx, ny = -ny, nz = -nz;
@@ -1398,6 +1399,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     // columns) -- state that would otherwise hold ~12 VGPRs through the walk
     double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
     uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);
+    uint4 *spec_lds = reinterpret_cast<uint4 *>(lane_stk + rtw_accel::kScratch * kThreads) + threadIdx.x;
     const double4 *sph = sv.sph;
     Tally tl;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1483,6 +1485,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         bool dry = false;  // wave-uniform: the cursor ran dry
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
         uint32_t x = 0, lr = 0, pseg = 0;
+        bool spec = false;  // spec_lds holds the state the lane's next unit vector draws from
         uint64_t pix = 0;
         PixelState ps;
         Path p;
@@ -1518,6 +1521,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     ps.k = 0;
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
+                    spec = false;
                     if (P.max_depth == 0) {  // every sample black, no Scene::hit call
                         ps.k = P.n_off;
                         write_pixel(P, x, lr, ps);
@@ -1560,7 +1564,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             double vx = 0., vy = 0., vz = 0.;
             if (kind != RTW_LAMBERTIAN) {  // unit(dir), vec3.rs:183-185
                 const double l = kMode == kBvh ? seg_sa : __builtin_sqrt(a);
-                vx = p.dx / l, vy = p.dy / l, vz = p.dz / l;
+                vx = p.dx, vy = p.dy, vz = p.dz;
+                rtw_num::div3(vx, vy, vz, l);  // / l, one shared reciprocal (rtw_numeric.h)
             }
             double cr = 0., cg = 0., cb = 0.;  // leaf colour of a sample that ends here
             bool ended = true;
@@ -1575,7 +1580,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 const ShadeRec M = sv.shd[best];
                 const double r = M.r;
                 const double hx = p.dx * bt + p.ox, hy = p.dy * bt + p.oy, hz = p.dz * bt + p.oz;
-                double nx = (hx - S.x) / r, ny = (hy - S.y) / r, nz = (hz - S.z) / r;
+                double nx = hx - S.x, ny = hy - S.y, nz = hz - S.z;
+                rtw_num::div3(nx, ny, nz, r);  // (p - c) / r
                 const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
                 if (!front) nx = -nx, ny = -ny, nz = -nz;
                 ended = p.depth + 1u >= P.max_depth;  // ray_color(depth >= max) -> black
@@ -1645,38 +1651,75 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             // judged in f32 first and rebuilt exactly only near the boundary
             const bool want_u = kind <= RTW_METAL;  // Lambertian or Metal
             const bool want_disk = ended && !done && !park && !(P.defocus_angle <= 0.);
+            // Speculation: a lane whose draws are done while others still loop goes on,
+            // on a copy of its RNG state, with the unit vector its NEXT segment will
+            // probably need (random_unit_vec's candidates do not depend on the
+            // geometry), and keeps the state its last try started from (the accepting
+            // try, or the next one). A Lambertian / Metal hit resumes from that state:
+            // the rejected tries are skipped, the same draws accepted. Anything else
+            // (the Schlick draw, the sky, the disk) goes on from the lane's own state.
+            if (spec && want_u) {
+                const uint4 r = *spec_lds;
+                ps.rng.lo = static_cast<uint64_t>(r.x) | static_cast<uint64_t>(r.y) << 32;
+                ps.rng.hi = static_cast<uint64_t>(r.z) | static_cast<uint64_t>(r.w) << 32;
+            }
+            const bool may_spec = !done && !park;  // the lane traces on from this state
+            // A lane's draws in order: phase 1 (its unit vector), 2 (the disk), 3 (the
+            // speculative unit vector of its next segment), 4 = finished. The wave loops
+            // while a lane is in phase 1 or 2; phase 3 never extends the loop.
             // The loop keeps only the accepted raw draws; their f64 coordinates are formed
             // once after it (inside it, only the rare candidates within 2^-17 of the
             // boundary need them, for the exact test).
-            uint32_t phase = want_u ? 1u : want_disk ? 2u : 0u;
+            const uint32_t after2 = may_spec ? 3u : 4u;
+            const uint32_t after1 = want_disk ? 2u : after2;
+            uint32_t phase = want_u ? 1u : after1;
             uint32_t um0 = 0, um1 = 0, um2 = 0, dm0 = 0, dm1 = 0;  // accepted draws (sphere, disk)
-            while (phase) {
+            U128 own = ps.rng, resume = ps.rng;  // the lane's own state; phase 3's resume point
+            bool did3 = phase == 3u;
+            bool any_real = __any(phase <= 2u);  // a lane leaves once finished; all, once no
+            while (any_real && phase <= 3u) {    // lane has a draw it needs
+                const U128 before = ps.rng;
+                const bool pu = phase != 2u;  // a unit-sphere try (1 or 3)
                 const uint32_t m0 = xs_next_m(ps.rng), m1 = xs_next_m(ps.rng);
                 uint32_t m2 = 0;
-                if (phase == 1u) m2 = xs_next_m(ps.rng);
-                const float x32 = coord32(m0), y32 = coord32(m1), z32 = phase == 1u ? coord32(m2) : 0.f;
+                if (pu) m2 = xs_next_m(ps.rng);
+                const float x32 = coord32(m0), y32 = coord32(m1), z32 = pu ? coord32(m2) : 0.f;
                 const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
                 bool ok = l32 < 1.f - kRejBand;  // surely accepted
                 if (!ok && !(l32 > 1.f + kRejBand)) {  // near the boundary: the exact test
                     const double x = coord64(m0), y = coord64(m1);
-                    if (phase == 1u) {
+                    if (pu) {
                         const double z = coord64(m2);
                         ok = x * x + y * y + z * z <= 1.;          // vec3.rs:219-226
                     } else {
                         ok = (x * x + y * y + 0. * 0.) < 1.;      // vec3.rs:270-277
                     }
                 }
-                if (ok) {
-                    if (phase == 1u) um0 = m0, um1 = m1, um2 = m2, phase = want_disk ? 2u : 0u;
-                    else dm0 = m0, dm1 = m1, phase = 0u;
-                }
+                // the bookkeeping as selects: no branch for the wave to pay
+                const bool a1 = ok && phase == 1u, a2 = ok && phase == 2u, a3 = ok && phase == 3u;
+                um0 = a1 ? m0 : um0, um1 = a1 ? m1 : um1, um2 = a1 ? m2 : um2;
+                dm0 = a2 ? m0 : dm0, dm1 = a2 ? m1 : dm1;
+                resume.lo = a3 ? before.lo : resume.lo, resume.hi = a3 ? before.hi : resume.hi;
+                const uint32_t next = a1 ? after1 : a2 ? after2 : a3 ? 4u : phase;
+                const bool enter3 = next == 3u && phase != 3u;
+                own.lo = enter3 ? ps.rng.lo : own.lo, own.hi = enter3 ? ps.rng.hi : own.hi;
+                did3 = did3 || enter3;
+                phase = next;
+                any_real = __any(phase <= 2u);
+            }
+            spec = did3;
+            if (did3) {  // keep the resume point, back to the lane's own state
+                if (phase == 3u) resume = ps.rng;  // still rejecting: resume with the next try
+                *spec_lds = make_uint4(static_cast<uint32_t>(resume.lo), static_cast<uint32_t>(resume.lo >> 32),
+                                       static_cast<uint32_t>(resume.hi), static_cast<uint32_t>(resume.hi >> 32));
+                ps.rng = own;
             }
             STAMP(9);  // 9: the draws
             double ux, uy, uz;
             if (want_u && !ended) {  // materials.rs:22-37 / 52-63 with u = unit(the point)
                 ux = coord64(um0), uy = coord64(um1), uz = coord64(um2);
                 const double l = __builtin_sqrt(ux * ux + uy * uy + uz * uz);
-                ux = ux / l, uy = uy / l, uz = uz / l;
+                rtw_num::div3(ux, uy, uz, l);  // u / l
                 double ndx = p.dx + ux * fz, ndy = p.dy + uy * fz, ndz = p.dz + uz * fz;
                 // near_zero without abs (vec3.rs:246-250): Lambertian falls back to n
                 if (kind == RTW_LAMBERTIAN && ndx < 1e-8 && ndy < 1e-8 && ndz < 1e-8) ndx = p.dx, ndy = p.dy, ndz = p.dz;
