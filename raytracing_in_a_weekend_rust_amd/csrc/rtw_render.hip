@@ -313,7 +313,10 @@ __device__ __forceinline__ uint64_t stamp_now() {
 }
 struct Stamps {
     uint64_t last = stamp_now(), acc[kStampSlots] = {};
+    uint64_t cnt[4] = {};  // draws loop (rows 10-13): [0] trips (max over lanes), [1] lanes needing
+                           // a unit vector, [2] of them resumed from a speculation, [3] needing the disk
 };
+#define STAMP_CNT(k, v) (stp.cnt[k] += (v))
 #define STAMP(k)                                   \
     do {                                           \
         const uint64_t t_ = stamp_now();           \
@@ -325,6 +328,7 @@ struct Stamps {};
 #define STAMP(k) \
     do {         \
     } while (0)
+#define STAMP_CNT(k, v) ((void)0)
 #endif
 
 // ---------------------------------------------------------------- megakernel --
@@ -1658,6 +1662,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             // try, or the next one). A Lambertian / Metal hit resumes from that state:
             // the rejected tries are skipped, the same draws accepted. Anything else
             // (the Schlick draw, the sky, the disk) goes on from the lane's own state.
+            STAMP_CNT(1, want_u ? 1u : 0u);
+            STAMP_CNT(2, spec && want_u ? 1u : 0u);
+            STAMP_CNT(3, want_disk ? 1u : 0u);
             if (spec && want_u) {
                 const uint4 r = *spec_lds;
                 ps.rng.lo = static_cast<uint64_t>(r.x) | static_cast<uint64_t>(r.y) << 32;
@@ -1678,6 +1685,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             bool did3 = phase == 3u;
             bool any_real = __any(phase <= 2u);  // a lane leaves once finished; all, once no
             while (any_real && phase <= 3u) {    // lane has a draw it needs
+                STAMP_CNT(0, 1u);
                 const U128 before = ps.rng;
                 const bool pu = phase != 2u;  // a unit-sphere try (1 or 3)
                 const uint32_t m0 = xs_next_m(ps.rng), m1 = xs_next_m(ps.rng);
@@ -1760,6 +1768,14 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             uint32_t wi = tl.witer;  // wave iterations (counted on one lane each)
             for (int off = 32; off > 0; off >>= 1) wi += static_cast<uint32_t>(__shfl_xor(static_cast<int>(wi), off));
             if (lane == 0) row[14] = wi, row[15] = stamp_now();
+            for (int k = 0; k < 4; ++k) {  // draws-loop counters: trips = max over lanes, the rest sums
+                uint64_t v = stp.cnt[k];
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v, off);
+                    v = k == 0 ? (v > o ? v : o) : v + o;
+                }
+                if (lane == 0) row[10 + k] = v;
+            }
         }
 #endif
         // this wave parks no more (its parks are published: drained stores + flags)

@@ -33,4 +33,5 @@ print(f"  total {tot.sum() / wi:.0f} cycles per wave-iteration (sections are max
 cnt = rows[:, 10:14].sum(axis=0).astype(np.float64)
 if cnt.any():
     print(f"draws loop: {cnt[0] / wi:.2f} wave trips per wave-iteration; per wave-iteration lanes needing a unit "
-          f"vector {cnt[1] / wi:.1f}, drawn by the speculation {cnt[2] / wi:.1f}, speculations discarded {cnt[3] / wi:.1f}")
+          f"vector {cnt[1] / wi:.1f}, of them resumed from a speculation {cnt[2] / wi:.1f}, lanes needing the disk "
+          f"{cnt[3] / wi:.1f}")
