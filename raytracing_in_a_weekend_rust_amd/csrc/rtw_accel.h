@@ -312,9 +312,8 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
 #if defined(__HIP_DEVICE_COMPILE__)
         // byte offset by a full-rate v_mul_u32_u24 (ids < 2^16; the compiler
         // otherwise picks the quarter-rate v_mul_lo_u32)
-        uint32_t off;
         static_assert(kNodeF4 * 16u == 144u, "node stride");
-        asm("v_mul_u32_u24 %0, 0x90, %1" : "=v"(off) : "v"(cur));
+        const uint32_t off = __umul24(cur, 144u);
         const F4 *N = reinterpret_cast<const F4 *>(reinterpret_cast<const char *>(nodes) + off);
 #else
         const F4 *N = nodes + kNodeF4 * cur;

@@ -1681,16 +1681,16 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const uint32_t after1 = want_disk ? 2u : after2;
             uint32_t phase = want_u ? 1u : after1;
             uint32_t um0 = 0, um1 = 0, um2 = 0, dm0 = 0, dm1 = 0;  // accepted draws (sphere, disk)
-            U128 own = ps.rng, resume = ps.rng;  // the lane's own state; phase 3's resume point
+            U128 own = ps.rng;  // the lane's own state (phase 3 runs on a copy)
             bool did3 = phase == 3u;
             bool any_real = __any(phase <= 2u);  // a lane leaves once finished; all, once no
             while (any_real && phase <= 3u) {    // lane has a draw it needs
                 STAMP_CNT(0, 1u);
-                const U128 before = ps.rng;
+                U128 st = ps.rng;
                 const bool pu = phase != 2u;  // a unit-sphere try (1 or 3)
-                const uint32_t m0 = xs_next_m(ps.rng), m1 = xs_next_m(ps.rng);
+                const uint32_t m0 = xs_next_m(st), m1 = xs_next_m(st);
                 uint32_t m2 = 0;
-                if (pu) m2 = xs_next_m(ps.rng);
+                if (pu) m2 = xs_next_m(st);
                 const float x32 = coord32(m0), y32 = coord32(m1), z32 = pu ? coord32(m2) : 0.f;
                 const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
                 bool ok = l32 < 1.f - kRejBand;  // surely accepted
@@ -1707,7 +1707,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 const bool a1 = ok && phase == 1u, a2 = ok && phase == 2u, a3 = ok && phase == 3u;
                 um0 = a1 ? m0 : um0, um1 = a1 ? m1 : um1, um2 = a1 ? m2 : um2;
                 dm0 = a2 ? m0 : dm0, dm1 = a2 ? m1 : dm1;
-                resume.lo = a3 ? before.lo : resume.lo, resume.hi = a3 ? before.hi : resume.hi;
+                // every try advances the state except phase 3's accepting one: that
+                // state (the try's start) is the resume point
+                ps.rng.lo = a3 ? ps.rng.lo : st.lo, ps.rng.hi = a3 ? ps.rng.hi : st.hi;
                 const uint32_t next = a1 ? after1 : a2 ? after2 : a3 ? 4u : phase;
                 const bool enter3 = next == 3u && phase != 3u;
                 own.lo = enter3 ? ps.rng.lo : own.lo, own.hi = enter3 ? ps.rng.hi : own.hi;
@@ -1716,10 +1718,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 any_real = __any(phase <= 2u);
             }
             spec = did3;
-            if (did3) {  // keep the resume point, back to the lane's own state
-                if (phase == 3u) resume = ps.rng;  // still rejecting: resume with the next try
-                *spec_lds = make_uint4(static_cast<uint32_t>(resume.lo), static_cast<uint32_t>(resume.lo >> 32),
-                                       static_cast<uint32_t>(resume.hi), static_cast<uint32_t>(resume.hi >> 32));
+            if (did3) {  // keep the resume point (the accepting try's start, or the next try's),
+                         // back to the lane's own state
+                *spec_lds = make_uint4(static_cast<uint32_t>(ps.rng.lo), static_cast<uint32_t>(ps.rng.lo >> 32),
+                                       static_cast<uint32_t>(ps.rng.hi), static_cast<uint32_t>(ps.rng.hi >> 32));
                 ps.rng = own;
             }
             STAMP(9);  // 9: the draws
