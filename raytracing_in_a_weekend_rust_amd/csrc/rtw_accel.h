@@ -207,16 +207,15 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
-    if (disc < r.negG) return;
-    ws.add_cand(k);
-    // sure hit iff disc > d2 - 2 negG (> 0: sd is then a real root; otherwise
-    // sd and slo are unused)
+    ws.add_cand(k, !(disc < r.negG));  // kept unless the filter proves a miss
+    // sure hit iff disc > d2 - 2 negG (> 0, so also kept; sd is then a real root;
+    // otherwise sd and slo are unused)
     const float sd = sqrt32(disc);
     const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
     const float sfar = sd - hb;
     const float slack = 1.953125e-3f * (fabsf(hb) + sd);  // 2^-9
     const bool sure = disc > d2 - 2.f * r.negG && slo - slack > r.tmin * 1.001f;
-    U = sure ? fminf(U, sfar + slack) : U;
+    U = fminf(U, sure ? sfar + slack : U);
 }
 
 // Walk scratch: the traversal stack of 16-bit node ids (LIFO) and the candidate
@@ -226,8 +225,9 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
 // puts every child slot far to near without branching, so up to 4 slots above
 // the kept entries are written. Invariant: kept + 4 + candidates <= kScratch
 // (else overflow: the caller brute-forces), at most kMaxCand candidates.
-// add_cand never exits the walk: a candidate that does not fit sets `bad` (its
-// store goes to the unclaimed next candidate slot, always inside the column).
+// add_cand never exits the walk and never branches: the leaf id is stored in the
+// unclaimed next candidate slot (always inside the column) and claimed if kept; a
+// kept candidate that does not fit sets `bad`.
 // next() ends the node: it records a stack overflow in `bad` and pops the next
 // node unless the stack is empty or the walk has failed -- the walk's one exit.
 constexpr uint32_t kScratch = 16;
@@ -246,11 +246,11 @@ struct ArrayScratch {
         id = e[--sp];
         return true;
     }
-    RTW_HD void add_cand(uint32_t k) {
+    RTW_HD void add_cand(uint32_t k, bool keep) {
         const bool ok = nc < kMaxCand && sp + 5u + nc <= kScratch;
         e[kScratch - 1u - nc] = static_cast<uint16_t>(k);
-        nc += ok ? 1u : 0u;
-        bad |= ok ? 0u : 1u;
+        nc += keep && ok ? 1u : 0u;
+        bad |= keep && !ok ? 1u : 0u;
     }
     RTW_HD uint32_t cand_at(uint32_t j) const { return e[kScratch - 1u - j]; }
 };
@@ -276,14 +276,14 @@ struct LdsScratch {
         id = *top;
         return true;
     }
-    __device__ void add_cand(uint32_t k) {
+    __device__ void add_cand(uint32_t k, bool keep) {
         const bool ok = nc < kMaxCand && top < lim;
-        *cand = static_cast<uint16_t>(k);
-        const uint32_t step = ok ? 2u * stride : 0u;  // bytes
+        *cand = static_cast<uint16_t>(k);  // claimed only if kept: else the next one overwrites it
+        const uint32_t step = keep && ok ? 2u * stride : 0u;  // bytes
         cand = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(cand) - step);
         lim = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lim) - step);
-        nc += ok ? 1u : 0u;
-        bad |= ok ? 0u : 1u;
+        nc += keep && ok ? 1u : 0u;
+        bad |= keep && !ok ? 1u : 0u;
     }
     __device__ uint32_t cand_at(uint32_t j) const { return base[(kScratch - 1u - j) * stride]; }
 };
