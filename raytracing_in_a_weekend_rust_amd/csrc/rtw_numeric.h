@@ -24,22 +24,22 @@ namespace rtw_num {
 // k = bitlen(m) - 21 bits of m; T > 0 only matters when those bits are a tie
 // (10...0), where the true value lies above the midpoint and the result must
 // round up -- RN-even rounds down there iff bit k of m is 0.
+// Branch-free (a wave runs it for a few lanes at a time): k is clamped to >= 1 and
+// the tie test is masked by b >= 22 instead of branched on.
 RTW_NHD double next01_of(uint32_t m) {
     const double A = static_cast<double>(m) * 0x1p-32;
     const double B = static_cast<double>(m) * 0x1p-64;
-    double s = A + B;
+    const double s = A + B;
     const uint32_t b = 32u - static_cast<uint32_t>(__builtin_clz(m | 1u));
-    if (b >= 22u) {
-        const uint32_t k = b - 21u;
-        const uint32_t low = m & ((1u << k) - 1u), half = 1u << (k - 1u);
-        if (low == half && !((m >> k) & 1u)) {
-            uint64_t u;
-            memcpy(&u, &s, 8);
-            ++u;
-            memcpy(&s, &u, 8);
-        }
-    }
-    return s;
+    const uint32_t k = (b >= 22u ? b : 22u) - 21u;
+    const uint32_t low = m & ((1u << k) - 1u), half = 1u << (k - 1u);
+    const bool up = b >= 22u && low == half && !((m >> k) & 1u);
+    uint64_t u;
+    memcpy(&u, &s, 8);
+    u += up ? 1u : 0u;
+    double r;
+    memcpy(&r, &u, 8);
+    return r;
 }
 
 // ---- f64 divisions by one divisor sharing its reciprocal (device) ----------
