@@ -118,6 +118,26 @@ def test_empty_scene_and_pinhole_camera():
     assert_same(fb, ref, st, seg)
 
 
+def test_walk_scratch_overflow_falls_back_exactly():
+    """A cluster of coincident spheres gives every ray through it more candidates
+    than the walk scratch holds (rtw_accel.h kMaxCand = 8): the walk records the
+    overflow without branching out, and the segment is redone by the scan -- same
+    (t, index) first minimum as the reference, bit-for-bit."""
+    world = rtw.SceneBuilder()
+    lam = rtw.Lambertian((0.5, 0.6, 0.7))
+    world.add(rtw.Sphere.new_world_obj(0., -100.5, -1., 100., rtw.Lambertian((0.8, 0.8, 0.))))
+    for _ in range(24):  # identical spheres: the first index wins every tie
+        world.add(rtw.Sphere.new_world_obj(0., 0., -1., 0.5, lam))
+    world.add(rtw.Sphere.new_world_obj(1., 0., -1., 0.5, rtw.Metal((0.8, 0.6, 0.2), 0.3)))
+    world.add(rtw.Sphere.new_world_obj(-1., 0., -1., 0.5, rtw.Dielectric(1.5)))
+    sph, n, mt, nm = world.build().flatten()
+    cam = rtw.Camera.new(24, 40, 12, 1.0, 60.0, (0., 0.3, 1.), (0., 0., -1.), (0., 1., 0.), 0.0, 1.0)
+    fb, st = gpu(cam, sph, n, mt, nm, 2, 17)
+    ref, seg = oracle(cam, sph, n, mt, nm, 2, 17)
+    assert_same(fb, ref, st, seg)
+    assert st.accel == 2 and st.brute_segments > 0
+
+
 def test_custom_scene_through_trait_surface(tmp_path):
     world = rtw.SceneBuilder()
     world.add(rtw.Sphere.new_world_obj(0., -100.5, -1., 100., rtw.Lambertian((0.8, 0.8, 0.0))))
