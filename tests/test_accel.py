@@ -48,6 +48,7 @@ def test_walk_matches_scan(exe, scene, seed, paths):
     assert r["bvh"], r
     assert r["mismatches"] == 0
     assert r["rays"] > paths
+    assert r["early_miss"] > r["early_tests"] // 20, r  # sphere_early_miss was exercised
     if scene == "complex":
         # the walk replaces the 486-sphere scan by ~20 node/leaf tests
         assert r["visits_per_walk"] < 40, r

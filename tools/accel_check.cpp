@@ -55,12 +55,13 @@ struct Hit {
     double t = 0.;
 };
 
+// the reference's scan with the plain Sphere::hit
 static Hit brute(const Scene &S, const double o[3], const double d[3]) {
     const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     Hit h;
     for (uint32_t i = 0; i < S.n; ++i) {
         double t;
-        if (sphere_hit_f64(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
+        if (sphere_hit_f64_plain(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
                            S.c[3 * i + 2], S.rr[i], t) &&
             (h.idx < 0 || t < h.t))
             h.idx = static_cast<int>(i), h.t = t;
@@ -70,7 +71,7 @@ static Hit brute(const Scene &S, const double o[3], const double d[3]) {
 
 struct Counts {
     uint64_t rays = 0, walked = 0, visits = 0, max_visits = 0, cands = 0, fallbacks = 0,
-             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0, inside = 0;
+             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0, inside = 0, early = 0, early_tests = 0;
 };
 
 // The kernel's accelerated Scene::hit, host-side. `prev` = the sphere the path
@@ -344,15 +345,58 @@ int main(int argc, char **argv) {
         for (int j = 0; j < 3; ++j) d[j] = (in * v[j] / vl + w[j] / wl) * sc;
         check(S, o, d, k, nullptr, static_cast<int>(i));
     }
+    // 5. sphere_early_miss (rtw_accel.h, opt-in): one sphere, origins on its surface
+    // (rounded, plus offsets of +-2^-k radii; odd p: inside by |c| ~ 2 R^2 delta with
+    // |d|^2 ~ |c| / 1.6e-5, the c < 0 bound's edge), directions outward / tangent /
+    // inward at scales 2^-60 .. 2^60: every early miss is a miss of the plain Sphere::hit
+    for (uint64_t p = 0; p < 4 * npaths && S.n; ++p) {
+        const uint32_t i = static_cast<uint32_t>(rng.next() % S.n);
+        const double R = std::fabs(S.r[i]);
+        double v[3], vl;
+        do {
+            v[0] = rng.sym(), v[1] = rng.sym(), v[2] = rng.sym();
+            vl = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        } while (vl > 1. || vl < 1e-3);
+        const double rad = R * (1. + (rng.u01() < 0.5 ? 0. : std::ldexp(rng.sym(), -static_cast<int>(rng.next() % 60))));
+        double o[3], d[3], w[3];
+        for (int j = 0; j < 3; ++j) o[j] = S.c[3 * i + j] + v[j] / vl * rad;
+        for (int j = 0; j < 3; ++j) w[j] = rng.sym();
+        const double mix = rng.u01() < 0.5 ? 1. : std::ldexp(rng.sym(), -static_cast<int>(rng.next() % 40));
+        double sc = std::ldexp(1., static_cast<int>(rng.next() % 121) - 60);
+        if (p & 1u) {
+            const double delta = std::ldexp(1., -1 - static_cast<int>(rng.next() % 50));
+            for (int j = 0; j < 3; ++j) o[j] = S.c[3 * i + j] + v[j] / vl * R * (1. - delta);
+            double l2 = 0.;
+            for (int j = 0; j < 3; ++j) l2 += (v[j] / vl * mix + w[j]) * (v[j] / vl * mix + w[j]);
+            sc = std::sqrt(2. * R * R * delta / 1.6e-5 * std::exp(2. * rng.sym()) / l2);
+        }
+        for (int j = 0; j < 3; ++j) d[j] = (v[j] / vl * mix + w[j]) * sc;
+        const double a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        const double ocx = o[0] - S.c[3 * i], ocy = o[1] - S.c[3 * i + 1], ocz = o[2] - S.c[3 * i + 2];
+        const double hb = ocx * d[0] + ocy * d[1] + ocz * d[2];
+        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - S.rr[i];
+        ++k.early_tests;
+        const bool early = sphere_early_miss(hb, c, a);
+        k.early += early ? 1u : 0u;
+        double t2 = 0.;
+        const bool h2 = sphere_hit_f64_plain(o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * i], S.c[3 * i + 1],
+                                             S.c[3 * i + 2], S.rr[i], t2);
+        if (early && h2) {
+            if (k.mismatches < 10)
+                fprintf(stderr, "EARLY-MISS MISMATCH sphere %u hb=%.17g c=%.17g a=%.17g t=%.17g\n", i, hb, c, a, t2);
+            ++k.mismatches;
+        }
+    }
     printf("{\"scene\": \"%s\", \"bvh\": true, \"n\": %u, \"always\": %zu, \"inner\": %u, \"depth\": %u, "
            "\"rays\": %llu, \"hits\": %llu, \"walked\": %llu, \"visits_per_walk\": %.3f, \"max_visits\": %llu, "
            "\"cands_per_walk\": %.3f, \"fallbacks\": %llu, \"overflows\": %llu, \"not_walkable\": %llu, "
-           "\"inside_cuts\": %llu, \"mismatches\": %llu}\n",
+           "\"inside_cuts\": %llu, \"early_miss\": %llu, \"early_tests\": %llu, \"mismatches\": %llu}\n",
            name.c_str(), S.n, S.bvh.always.size(), S.bvh.n_node, S.bvh.depth, (unsigned long long)k.rays,
            (unsigned long long)k.hits, (unsigned long long)k.walked,
            k.walked ? double(k.visits) / k.walked : 0., (unsigned long long)k.max_visits,
            k.walked ? double(k.cands) / k.walked : 0., (unsigned long long)k.fallbacks,
            (unsigned long long)k.overflows, (unsigned long long)k.not_walkable,
-           (unsigned long long)k.inside, (unsigned long long)k.mismatches);
+           (unsigned long long)k.inside, (unsigned long long)k.early, (unsigned long long)k.early_tests,
+           (unsigned long long)k.mismatches);
     return k.mismatches ? 1 : 0;
 }
