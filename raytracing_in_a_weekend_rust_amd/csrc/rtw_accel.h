@@ -219,6 +219,47 @@ RTW_HD bool slab_hit(float nx, float ny, float nz, float fx, float fy, float fz,
     return fmaxf(tn, r.tmin) <= fminf(tf, U);
 }
 
+// The four children's slab tests of one node as a hit mask (bit j = child j).
+// Opt-in RTW_PK_SLAB: the 24 plane FMAs as 12 v_pk_fma_f32 (children 0/1 and 2/3
+// in the halves of a register pair; each half the same IEEE fused multiply-add,
+// the same bits). Measured slower (parity +2.8 %, fast mode +5 %): a packed pair
+// occupies the SIMD as long as two plain f32 FMAs on gfx950, and the broadcast
+// ray constants take 9 more VGPRs (profiles/r02_misc/ab_pk_slab_REJECTED.log).
+template <typename F4>
+RTW_HD uint32_t slab_hit4(const F4 &nX, const F4 &nY, const F4 &nZ, const F4 &fX, const F4 &fY,
+                          const F4 &fZ, const WalkRay &r, float U) {
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RTW_PK_SLAB)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+    const f2 anx = {r.anx, r.anx}, any = {r.any, r.any}, anz = {r.anz, r.anz};
+    const f2 afx = {r.afx, r.afx}, afy = {r.afy, r.afy}, afz = {r.afz, r.afz};
+    uint32_t hit = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const f2 px = h ? f2{nX.z, nX.w} : f2{nX.x, nX.y}, py = h ? f2{nY.z, nY.w} : f2{nY.x, nY.y},
+                 pz = h ? f2{nZ.z, nZ.w} : f2{nZ.x, nZ.y};
+        const f2 qx = h ? f2{fX.z, fX.w} : f2{fX.x, fX.y}, qy = h ? f2{fY.z, fY.w} : f2{fY.x, fY.y},
+                 qz = h ? f2{fZ.z, fZ.w} : f2{fZ.x, fZ.y};
+        const f2 tnx = __builtin_elementwise_fma(px, ix, anx), tny = __builtin_elementwise_fma(py, iy, any),
+                 tnz = __builtin_elementwise_fma(pz, iz, anz);
+        const f2 tfx = __builtin_elementwise_fma(qx, ix, afx), tfy = __builtin_elementwise_fma(qy, iy, afy),
+                 tfz = __builtin_elementwise_fma(qz, iz, afz);
+        const float tn0 = fmax3(tnx.x, tny.x, tnz.x), tn1 = fmax3(tnx.y, tny.y, tnz.y);
+        const float tf0 = fmin3(tfx.x, tfy.x, tfz.x), tf1 = fmin3(tfx.y, tfy.y, tfz.y);
+        hit |= (fmaxf(tn0, r.tmin) <= fminf(tf0, U) ? 1u : 0u) << (2 * h);
+        hit |= (fmaxf(tn1, r.tmin) <= fminf(tf1, U) ? 2u : 0u) << (2 * h);
+    }
+    return hit;
+#else
+    uint32_t hit = 0;
+    hit |= slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, U) ? 1u : 0u;
+    hit |= slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, U) ? 2u : 0u;
+    hit |= slab_hit(nX.z, nY.z, nZ.z, fX.z, fY.z, fZ.z, r, U) ? 4u : 0u;
+    hit |= slab_hit(nX.w, nY.w, nZ.w, fX.w, fY.w, fZ.w, r, U) ? 8u : 0u;
+    return hit;
+#endif
+}
+
 // The pass-1 filter on leaf k; a kept sphere joins the candidate list (an
 // overflow is recorded in the scratch, the walk stops after the node) and, if it
 // is a sure hit (disc beyond the filter's inflation + error, far root clearly past
@@ -348,11 +389,7 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         // near / far planes picked by address (per-ray direction signs): no min/max
         const F4 nX = N[sx], fX = N[sx ^ 1u], nY = N[2u + sy], fY = N[3u - sy], nZ = N[4u + sz],
                  fZ = N[5u - sz], qc = N[6], qo = N[7];
-        uint32_t hit = 0;
-        hit |= slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, U) ? 1u : 0u;
-        hit |= slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, U) ? 2u : 0u;
-        hit |= slab_hit(nX.z, nY.z, nZ.z, fX.z, fY.z, fZ.z, r, U) ? 4u : 0u;
-        hit |= slab_hit(nX.w, nY.w, nZ.w, fX.w, fY.w, fZ.w, r, U) ? 8u : 0u;
+        uint32_t hit = slab_hit4(nX, nY, nZ, fX, fY, fZ, r, U);
         const uint32_t r01 = as_u32(qc.x), r23 = as_u32(qc.y), masks = as_u32(qc.z);
         hit &= masks;
         // leaf children first: they may tighten U for the inner children

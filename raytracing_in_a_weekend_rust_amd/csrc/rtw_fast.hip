@@ -168,10 +168,7 @@ __device__ __forceinline__ void scene_hit(const FastParams &P, const float4 *__r
         const float4 nX = N[sx], fX = N[sx ^ 1u], nY = N[2u + sy], fY = N[3u - sy], nZ = N[4u + sz],
                      fZ = N[5u - sz], qc = N[6], qo = N[7];
         uint32_t hit = 0;
-        hit |= rtw_accel::slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, best) ? 1u : 0u;
-        hit |= rtw_accel::slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, best) ? 2u : 0u;
-        hit |= rtw_accel::slab_hit(nX.z, nY.z, nZ.z, fX.z, fY.z, fZ.z, r, best) ? 4u : 0u;
-        hit |= rtw_accel::slab_hit(nX.w, nY.w, nZ.w, fX.w, fY.w, fZ.w, r, best) ? 8u : 0u;
+        hit |= rtw_accel::slab_hit4(nX, nY, nZ, fX, fY, fZ, r, best);
         const uint32_t r01w = rtw_accel::as_u32(qc.x), r23w = rtw_accel::as_u32(qc.y);
         const uint32_t masks = rtw_accel::as_u32(qc.z);
         hit &= masks;
