@@ -118,7 +118,9 @@ struct KParams {
     double defocus_angle;
     uint32_t W, s, n_off, max_depth;
     uint32_t row_begin, row_step, n_rows, n_sph;
-    uint32_t jump_bits, _pad;
+    uint32_t jump_bits;
+    uint32_t att_finite;        // every Lambertian / Metal albedo is finite: a black leaf (depth
+                                // cap) makes the sample's product +-0, an exact no-op in the sum
     uint32_t n_node, n_leaf, n_always, seg_budget;
     uint32_t order, heavy_per_block;
     uint32_t rate_k, rate_x;    // park a cursor pixel after rate_k samples above rate_x seg/sample
@@ -732,7 +734,10 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         }
         STAMP(3);  // 3: hit record + scatter / sky
         if (done) {
-            fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
+            // a depth-capped (or fast-forwarded) path's product is att x ... x 0 = +-0 with
+            // finite attenuations, and adding +-0 to the sum changes no bit: no fold
+            if (best >= 0 && KP(att_finite)) p.stk.clear();
+            else fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
             if (++ps.k >= n_off) break;
             if (seg >= budget) return true;  // sample boundary: hand the rest to the coop kernel
             gen_ray(P, pl, ps.k, ps.rng, p, stp);
@@ -1627,8 +1632,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             STAMP(6);  // 6: hit record + scatter without draws
             bool done = false, park = false;
             if (ended) {
-                fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
-                acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
+                if (best >= 0 && KP(att_finite)) {  // black leaf: +-0, no fold (see trace_samples)
+                    p.stk.clear();
+                } else {
+                    fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
+                    acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
+                }
                 done = ++ps.k >= P.n_off;
                 // park: the budget is spent, the rate runs away, or -- once the
                 // cursor is dry, so drain groups are about to be plentiful -- the
@@ -1973,6 +1982,7 @@ struct rtw_session {
     uint32_t *d_always = nullptr;
     uint32_t n_node = 0, n_leaf = 0, n_always = 0;
     bool has_bvh = false;
+    bool att_finite = true;  // every Lambertian / Metal albedo component finite (KParams::att_finite)
     uint32_t bvh_depth = 0;
     // f32 fast mode (rtw_fast.h): per-sphere geometry / material rows / kinds
     float4 *d_fgeo = nullptr, *d_fmat = nullptr;
@@ -2156,6 +2166,12 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         HIPCHECK(hipMemcpy(s->d_fmat, fm.data(), fm.size() * sizeof(float4), hipMemcpyHostToDevice));
         HIPCHECK(hipMemcpy(s->d_fkind, fk.data(), fk.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
+    s->att_finite = true;
+    for (uint32_t i = 0; i < n; ++i) {
+        const rtw_material &M = m[sp[i].mat];
+        if (M.kind != RTW_DIELECTRIC)
+            for (int k = 0; k < 3; ++k) s->att_finite = s->att_finite && std::isfinite(M.albedo[k]);
+    }
     s->n_sph = n;
     s->n_mats = nm;
     s->scene_set = true;
@@ -2236,6 +2252,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.leaves = s->d_leaves;
     P.always = s->d_always;
     P.jump_bits = bits;
+    P.att_finite = (s->att_finite && !std::getenv("RTW_FOLD_BLACK")) ? 1u : 0u;
     P.seed_lo = seed.lo;
     P.seed_hi = seed.hi;
     P.sph = s->d_sph;

@@ -243,7 +243,8 @@ def test_strategies_on_stress_and_deep_scenes(monkeypatch, tmp_path, accel, budg
     monkeypatch.setenv("RTW_BUDGET_X", budget)
     monkeypatch.setenv("RTW_COOP", coop)
     test_filter_stress_scenes()
-    test_deep_paths_use_spill_levels()
+    _deep_closed_sphere()
+    _escaping_mirrors()
     test_custom_scene_through_trait_surface(tmp_path)
 
 
@@ -315,9 +316,24 @@ def test_stress_config5_sampled_rows():
     assert_same(fb, ref, st, seg)
 
 
-def test_deep_paths_use_spill_levels():
+def _set_fold_black(monkeypatch, fold_black):
+    if fold_black:
+        monkeypatch.setenv("RTW_FOLD_BLACK", fold_black)
+    else:
+        monkeypatch.delenv("RTW_FOLD_BLACK", raising=False)
+
+
+@pytest.mark.parametrize("fold_black", ["", "1"])
+def test_deep_paths_use_spill_levels(monkeypatch, fold_black):
     """Camera inside a closed Lambertian sphere: every path bounces to the depth
-    cap, so the path stack runs past its register slots into the HBM spill levels."""
+    cap, so the path stack runs past its register slots into the HBM spill levels.
+    By default a depth-capped sample skips the fold (its product is +-0);
+    RTW_FOLD_BLACK=1 folds it through the spill levels as the recursion would."""
+    _set_fold_black(monkeypatch, fold_black)
+    _deep_closed_sphere()
+
+
+def _deep_closed_sphere():
     world = rtw.SceneBuilder()
     world.add(rtw.Sphere.new_world_obj(0., 0., 0., 10., rtw.Lambertian((0.93, 0.91, 0.97))))
     world.add(rtw.Sphere.new_world_obj(0., -1., -3., 1., rtw.Metal((0.8, 0.85, 0.9), 0.2)))
@@ -330,6 +346,33 @@ def test_deep_paths_use_spill_levels():
         ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, 31)
         assert_same(fb, ref, st, seg)
         assert st.segments == st.samples * depth  # nothing ever escapes
+
+
+@pytest.mark.parametrize("fold_black", ["", "1"])
+def test_long_escaping_paths_fold_spill_levels(monkeypatch, fold_black):
+    """Two big facing mirrors (r = 1e4, fuzz 0 and 0.05, 2 apart) with the camera
+    between them looking down at a slant: paths bounce ~20 times and most escape, so
+    the fold of a sky leaf reads its deepest attenuation rows back from the HBM spill
+    levels; the rest hit the depth cap (black leaf, fold skipped unless
+    RTW_FOLD_BLACK=1)."""
+    _set_fold_black(monkeypatch, fold_black)
+    _escaping_mirrors()
+
+
+def _escaping_mirrors():
+    world = rtw.SceneBuilder()
+    world.add(rtw.Sphere.new_world_obj(0., -10001., 0., 1e4, rtw.Metal((0.97, 0.95, 0.9), 0.)))
+    world.add(rtw.Sphere.new_world_obj(0., 10001., 0., 1e4, rtw.Metal((0.9, 0.95, 0.97), 0.05)))
+    world.add(rtw.Sphere.new_world_obj(0., 0., -4., 0.6, rtw.Lambertian((0.7, 0.3, 0.3))))
+    scene = world.build()
+    sph, n, mt, nm = scene.flatten()
+    cam = rtw.Camera.new(24, 40, 40, 1.0, 70.0, (0., 0., 0.), (0., -1., -3.), (0., 0., -1.), 0.2, 4.0)
+    fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, 3, 77)
+    ref, seg = orc.render(cam.raw, sph, n, mt, nm, 3, 77)
+    assert_same(fb, ref, st, seg)
+    assert st.segments > 12 * st.samples  # deep paths (~20 segments/sample): past the 8 register levels
+    assert float(ref.mean()) > 0.2  # most escape to the sky
+    assert float((ref.sum(-1) == 0).mean()) > 0.01  # some pixels only ever reach the depth cap
 
 
 @pytest.mark.parametrize("budget", ["0.01", "0"])
