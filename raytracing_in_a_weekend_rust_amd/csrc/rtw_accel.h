@@ -134,6 +134,22 @@ RTW_HD bool sphere_hit_f64(double ox, double oy, double oz, double dx, double dy
     return t >= 0.01;
 }
 
+// The sphere a segment starts on, as a leaf the walk may drop: a ray leaving it
+// (sphere_early_miss on the exact hb and c that sphere_hit_f64 computes, same
+// operations) cannot hit it at t >= 0.01, so the scan's minimum is the same
+// without it. Every bounce off a BVH sphere used to carry it as a candidate and an
+// exact f64 test (sqrt and both divisions). Returns the leaf id or 0xffff. Opt-in
+// on the device (RTW_SELF_SKIP): 37 % fewer candidates, but the wave's candidate
+// loop runs for its busiest lane's real candidates and the f64 check costs more
+// (+0.8 %, profiles/r02_misc/ab_self_skip_REJECTED.log); the host check uses it.
+RTW_HD uint32_t self_skip(int prev, double ox, double oy, double oz, double dx, double dy, double dz,
+                          double a, double cx, double cy, double cz, double rr) {
+    const double ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const double hb = ocx * dx + ocy * dy + ocz * dz;
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rr;
+    return prev >= 0 && sphere_early_miss(hb, c, a) ? static_cast<uint32_t>(prev) : 0xffffu;
+}
+
 // Exact-conservative f32 pre-filter of the discriminant (DESIGN.md "Exact
 // pre-filter"): records carry R2' >= r*r + K (m_c^2 + r*r/2) (host, rounded up)
 // and a lane with origin magnitude m_o keeps a sphere unless disc32 < -G,
@@ -158,6 +174,7 @@ struct WalkRay {
     float tmin;         // 0.01 |d| rounded down (distance units)
     float negG;         // -(filter margin G)
     uint32_t neg;       // bit k: e32 component k < 0 (near child = right on that axis)
+    uint32_t skip;      // a leaf the walk never keeps (self_skip), 0xffff: none
 };
 
 RTW_HD float clamp_dir(float e) {
@@ -173,6 +190,7 @@ RTW_HD bool walk_setup(float ox, float oy, float oz, float ex, float ey, float e
     if (!(fabsf(ex) <= 2.f) || !(fabsf(ey) <= 2.f) || !(fabsf(ez) <= 2.f)) return false;
     r.ox = ox, r.oy = oy, r.oz = oz, r.ex = ex, r.ey = ey, r.ez = ez;
     r.neg = (ex < 0.f ? 1u : 0u) | (ey < 0.f ? 2u : 0u) | (ez < 0.f ? 4u : 0u);
+    r.skip = 0xffffu;
     r.ix = rcp32(clamp_dir(ex)), r.iy = rcp32(clamp_dir(ey)), r.iz = rcp32(clamp_dir(ez));
     const float pad = kPadK * static_cast<float>(mo) + 1e-30f;
     // lo-plane offset -(o + pad) inv, hi-plane offset -(o - pad) inv; for a
@@ -275,7 +293,7 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
-    ws.add_cand(k, !(disc < r.negG));  // kept unless the filter proves a miss
+    ws.add_cand(k, !(disc < r.negG) && k != r.skip);  // kept unless the filter proves a miss
     // sure hit iff disc > d2 - 2 negG (> 0, so also kept; sd is then a real root;
     // otherwise sd and slo are unused)
     const float sd = sqrt32(disc);

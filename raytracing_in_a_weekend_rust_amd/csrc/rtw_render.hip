@@ -905,6 +905,12 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
             brute = true;
         } else {
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
+#ifdef RTW_SELF_SKIP  // opt-in: measured +0.8 % (the wave's candidate loop is set by real candidates)
+            {  // the sphere the segment leaves is no candidate (rtw_accel.h self_skip)
+                const double4 S = sph[prev >= 0 ? prev : 0];
+                wr.skip = rtw_accel::self_skip(prev, ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w);
+            }
+#endif
             auto run = [&](auto &ws) {
                 const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
                 STAMP(2);  // 2: BVH walk

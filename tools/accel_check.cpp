@@ -71,7 +71,7 @@ static Hit brute(const Scene &S, const double o[3], const double d[3]) {
 
 struct Counts {
     uint64_t rays = 0, walked = 0, visits = 0, max_visits = 0, cands = 0, fallbacks = 0,
-             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0, inside = 0, early = 0, early_tests = 0;
+             overflows = 0, not_walkable = 0, mismatches = 0, hits = 0, inside = 0, early = 0, early_tests = 0, self_skips = 0;
 };
 
 // The kernel's accelerated Scene::hit, host-side. `prev` = the sphere the path
@@ -116,6 +116,12 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
         return brute(S, o, d);
     }
     ++k.walked;
+    if (prev >= 0) {  // the device drops the sphere a segment leaves (rtw_accel.h self_skip)
+        const uint32_t p = static_cast<uint32_t>(prev);
+        wr.skip = self_skip(prev, o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * p], S.c[3 * p + 1], S.c[3 * p + 2],
+                            S.rr[p]);
+        k.self_skips += wr.skip != 0xffffu ? 1u : 0u;
+    }
     float U = INFINITY;
     if (h.idx >= 0) U = seed_cut(h.t, sa);
     uint32_t visits = 0;
@@ -390,13 +396,13 @@ int main(int argc, char **argv) {
     printf("{\"scene\": \"%s\", \"bvh\": true, \"n\": %u, \"always\": %zu, \"inner\": %u, \"depth\": %u, "
            "\"rays\": %llu, \"hits\": %llu, \"walked\": %llu, \"visits_per_walk\": %.3f, \"max_visits\": %llu, "
            "\"cands_per_walk\": %.3f, \"fallbacks\": %llu, \"overflows\": %llu, \"not_walkable\": %llu, "
-           "\"inside_cuts\": %llu, \"early_miss\": %llu, \"early_tests\": %llu, \"mismatches\": %llu}\n",
+           "\"inside_cuts\": %llu, \"self_skips\": %llu, \"early_miss\": %llu, \"early_tests\": %llu, \"mismatches\": %llu}\n",
            name.c_str(), S.n, S.bvh.always.size(), S.bvh.n_node, S.bvh.depth, (unsigned long long)k.rays,
            (unsigned long long)k.hits, (unsigned long long)k.walked,
            k.walked ? double(k.visits) / k.walked : 0., (unsigned long long)k.max_visits,
            k.walked ? double(k.cands) / k.walked : 0., (unsigned long long)k.fallbacks,
            (unsigned long long)k.overflows, (unsigned long long)k.not_walkable,
-           (unsigned long long)k.inside, (unsigned long long)k.early, (unsigned long long)k.early_tests,
+           (unsigned long long)k.inside, (unsigned long long)k.self_skips, (unsigned long long)k.early, (unsigned long long)k.early_tests,
            (unsigned long long)k.mismatches);
     return k.mismatches ? 1 : 0;
 }
