@@ -293,7 +293,11 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
+#if !defined(__HIP_DEVICE_COMPILE__) || defined(RTW_SELF_SKIP)
     ws.add_cand(k, !(disc < r.negG) && k != r.skip);  // kept unless the filter proves a miss
+#else
+    ws.add_cand(k, !(disc < r.negG));  // kept unless the filter proves a miss
+#endif
     // sure hit iff disc > d2 - 2 negG (> 0, so also kept; sd is then a real root;
     // otherwise sd and slo are unused)
     const float sd = sqrt32(disc);
