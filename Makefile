@@ -4,7 +4,10 @@
 # with the reference's generic x86-64 release build depends on it.
 HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
-ARCH ?= gfx950
+# xnack- : the pool runs without XNACK (no page-fault retry), and code built for it is
+# free of the xnack-any constraints: 127.9 -> 127.5 ms per image, 8-round A/B
+# (profiles/r02_misc/ab_xnack_off.log)
+ARCH ?= gfx950:xnack-
 PKG := raytracing_in_a_weekend_rust_amd
 SRC := $(PKG)/csrc
 OUT := $(PKG)/_lib
