@@ -1989,6 +1989,13 @@ struct rtw_session {
     uint32_t n_node = 0, n_leaf = 0, n_always = 0;
     bool has_bvh = false;
     bool att_finite = true;  // every Lambertian / Metal albedo component finite (KParams::att_finite)
+    // the scene's device tables live in one grow-only arena, uploaded with one copy
+    // (d_sph, d_filt, d_shade, d_nbr, d_trap, d_nodes, d_leaves, d_always, d_fgeo,
+    // d_fmat and d_fkind point into it)
+    char *d_arena = nullptr;
+    size_t arena_cap = 0;
+    void *d_out = nullptr;  // the one-shot API's framebuffer (grow-only)
+    size_t out_cap = 0;
     uint32_t bvh_depth = 0;
     // f32 fast mode (rtw_fast.h): per-sphere geometry / material rows / kinds
     float4 *d_fgeo = nullptr, *d_fmat = nullptr;
@@ -2033,13 +2040,36 @@ void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uin
         if (sp[i].mat >= nm) throw rtw::Error(RTW_E_MAT_INDEX, "sphere material index out of range");
 }
 
+// Host staging of the scene tables: each table at a 256-B aligned offset of one
+// buffer, copied to the session's arena in one transfer (a dozen hipMalloc /
+// hipFree / hipMemcpy round trips per scene before).
+struct SceneStage {
+    std::vector<char> host;
+    std::vector<std::pair<void **, size_t>> slots;
+    template <class T>
+    void add(T **slot, const T *src, size_t count) {
+        const size_t off = (host.size() + 255) & ~static_cast<size_t>(255);
+        host.resize(off + std::max<size_t>(count * sizeof(T), 16));
+        if (count) std::memcpy(host.data() + off, src, count * sizeof(T));
+        slots.emplace_back(reinterpret_cast<void **>(slot), off);
+    }
+    void upload(rtw_session *s) {
+        if (host.size() > s->arena_cap) {
+            dev_free(s->d_arena);
+            s->d_arena = nullptr, s->arena_cap = 0;
+            HIPCHECK(hipMalloc(&s->d_arena, host.size()));
+            s->arena_cap = host.size();
+        }
+        HIPCHECK(hipMemcpy(s->d_arena, host.data(), host.size(), hipMemcpyHostToDevice));
+        for (auto &sl : slots) *sl.first = s->d_arena + sl.second;
+    }
+};
+
 void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
     validate_scene(sp, n, m, nm);
     HIPCHECK(hipSetDevice(s->device));
-    dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_shade), dev_free(s->d_nbr), dev_free(s->d_trap);
-    dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
-    dev_free(s->d_fgeo), dev_free(s->d_fmat), dev_free(s->d_fkind);
+    if (s->pending) HIPCHECK(hipEventSynchronize(s->ev1));  // a render may still read the arena
+    SceneStage stage;
     s->d_fgeo = s->d_fmat = nullptr, s->d_fkind = nullptr;
     s->d_sph = nullptr, s->d_filt = nullptr;
     s->d_shade = nullptr, s->d_nbr = nullptr, s->n_nbr = 0, s->d_trap = nullptr;
@@ -2107,19 +2137,14 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         rtw_accel::build_inside(cen.data(), rad.data(), n, info, nbr_ids, trap_ok.data(), &traps);
         for (uint32_t i = 0; i < n; ++i) sh[i].nbr = info[i];
         static_assert(sizeof(rtw_accel::TrapRec) == sizeof(double4), "TrapRec layout");
-        HIPCHECK(hipMalloc(&s->d_trap, (n ? n : 1) * sizeof(double4)));
-        if (n) HIPCHECK(hipMemcpy(s->d_trap, traps.data(), n * sizeof(double4), hipMemcpyHostToDevice));
+        stage.add(reinterpret_cast<rtw_accel::TrapRec **>(&s->d_trap), traps.data(), n);
     }
-    HIPCHECK(hipMalloc(&s->d_nbr, (nbr_ids.size() + 8) * sizeof(uint16_t)));
-    if (!nbr_ids.empty())
-        HIPCHECK(hipMemcpy(s->d_nbr, nbr_ids.data(), nbr_ids.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-    s->n_nbr = static_cast<uint32_t>(nbr_ids.size());
-    HIPCHECK(hipMalloc(&s->d_sph, a.size() * sizeof(double4)));
-    HIPCHECK(hipMalloc(&s->d_filt, f.size() * sizeof(float4)));
-    HIPCHECK(hipMalloc(&s->d_shade, sh.size() * sizeof(ShadeRec)));
-    HIPCHECK(hipMemcpy(s->d_sph, a.data(), a.size() * sizeof(double4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_filt, f.data(), f.size() * sizeof(float4), hipMemcpyHostToDevice));
-    HIPCHECK(hipMemcpy(s->d_shade, sh.data(), sh.size() * sizeof(ShadeRec), hipMemcpyHostToDevice));
+    nbr_ids.resize(nbr_ids.size() + 8, 0);  // padded (staged like the old allocation)
+    stage.add(&s->d_nbr, nbr_ids.data(), nbr_ids.size());
+    s->n_nbr = static_cast<uint32_t>(nbr_ids.size() - 8);
+    stage.add(&s->d_sph, a.data(), a.size());
+    stage.add(&s->d_filt, f.data(), f.size());
+    stage.add(&s->d_shade, sh.data(), sh.size());
     // BVH over the same records (rtw_accel_build.cpp); ineligible scenes scan
     {
         std::vector<double> cen(3 * static_cast<size_t>(n)), rad(n);
@@ -2131,15 +2156,12 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         }
         rtw_accel::Bvh bvh;
         if (n && rtw_accel::build(cen.data(), rad.data(), r2p.data(), n, bvh)) {
-            const size_t nb = bvh.nodes.size() * sizeof(float), lb = bvh.leaves.size() * sizeof(float);
-            HIPCHECK(hipMalloc(&s->d_nodes, nb ? nb : 16));
-            HIPCHECK(hipMalloc(&s->d_leaves, lb ? lb : 16));
-            HIPCHECK(hipMalloc(&s->d_always, (bvh.always.size() + 1) * sizeof(uint32_t)));
-            if (nb) HIPCHECK(hipMemcpy(s->d_nodes, bvh.nodes.data(), nb, hipMemcpyHostToDevice));
-            if (lb) HIPCHECK(hipMemcpy(s->d_leaves, bvh.leaves.data(), lb, hipMemcpyHostToDevice));
-            if (!bvh.always.empty())
-                HIPCHECK(hipMemcpy(s->d_always, bvh.always.data(), bvh.always.size() * sizeof(uint32_t),
-                                   hipMemcpyHostToDevice));
+            static_assert(sizeof(float4) == 4 * sizeof(float), "node layout");
+            stage.add(&s->d_nodes, reinterpret_cast<const float4 *>(bvh.nodes.data()), bvh.nodes.size() / 4);
+            stage.add(&s->d_leaves, reinterpret_cast<const float4 *>(bvh.leaves.data()), bvh.leaves.size() / 4);
+            bvh.always.push_back(0u);  // one spare entry, as the old allocation had
+            stage.add(&s->d_always, bvh.always.data(), bvh.always.size());
+            bvh.always.pop_back();
             s->n_node = bvh.n_node, s->n_leaf = bvh.n_leaf;
             s->n_always = static_cast<uint32_t>(bvh.always.size());
             s->bvh_depth = bvh.depth;
@@ -2165,13 +2187,11 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
             }
             fk[i] = M.kind;
         }
-        HIPCHECK(hipMalloc(&s->d_fgeo, fg.size() * sizeof(float4)));
-        HIPCHECK(hipMalloc(&s->d_fmat, fm.size() * sizeof(float4)));
-        HIPCHECK(hipMalloc(&s->d_fkind, fk.size() * sizeof(uint32_t)));
-        HIPCHECK(hipMemcpy(s->d_fgeo, fg.data(), fg.size() * sizeof(float4), hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(s->d_fmat, fm.data(), fm.size() * sizeof(float4), hipMemcpyHostToDevice));
-        HIPCHECK(hipMemcpy(s->d_fkind, fk.data(), fk.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        stage.add(&s->d_fgeo, fg.data(), fg.size());
+        stage.add(&s->d_fmat, fm.data(), fm.size());
+        stage.add(&s->d_fkind, fk.data(), fk.size());
     }
+    stage.upload(s);
     s->att_finite = true;
     for (uint32_t i = 0; i < n; ++i) {
         const rtw_material &M = m[sp[i].mat];
@@ -2737,7 +2757,6 @@ int threaded(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_sphere
     static std::mutex mu;
     static rtw_session *cached = nullptr;
     std::lock_guard<std::mutex> lock(mu);
-    T *d_out = nullptr;
     RTW_GUARD_BEGIN
     if (cam->img_height == 0 || cam->img_width == 0)
         throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
@@ -2748,25 +2767,19 @@ int threaded(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_sphere
     if (!cached) create_session(dev, &cached);
     set_scene(cached, spheres, n_spheres, mats, n_mats);
     const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(T);
-    HIPCHECK(hipMalloc(&d_out, bytes ? bytes : 8));
+    if (std::max<size_t>(bytes, 8) > cached->out_cap) {  // grow-only device framebuffer
+        dev_free(cached->d_out);
+        cached->d_out = nullptr, cached->out_cap = 0;
+        HIPCHECK(hipMalloc(&cached->d_out, std::max<size_t>(bytes, 8)));
+        cached->out_cap = std::max<size_t>(bytes, 8);
+    }
+    T *d_out = static_cast<T *>(cached->d_out);
     run(cached, &sh, d_out, cached->own);
     collect(cached);
     if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
-    HIPCHECK(hipFree(d_out));
-    d_out = nullptr;
     if (stats) *stats = cached->last;
     return RTW_OK;
-    }
-    catch (const rtw::Error &e) {
-        if (d_out) (void)hipFree(d_out);
-        rtw::set_error(e.what());
-        return e.code;
-    }
-    catch (const std::exception &e) {
-        if (d_out) (void)hipFree(d_out);
-        rtw::set_error(e.what());
-        return RTW_E_ARG;
-    }
+    RTW_GUARD_END
 }
 
 extern "C" {
@@ -2791,14 +2804,12 @@ int rtw_session_destroy(rtw_session *s) {
     if (!s) return RTW_OK;
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
-    dev_free(s->d_sph), dev_free(s->d_filt);
-    dev_free(s->d_shade), dev_free(s->d_nbr), dev_free(s->d_trap);
+    dev_free(s->d_arena), dev_free(s->d_out);  // the scene tables point into the arena
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
-    dev_free(s->d_nodes), dev_free(s->d_leaves), dev_free(s->d_always);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
     dev_free(s->d_pcost), dev_free(s->d_err);
-    dev_free(s->d_fgeo), dev_free(s->d_fmat), dev_free(s->d_fkind), dev_free(s->d_fcursor), dev_free(s->d_fcount);
+    dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     if (s->own) (void)hipStreamDestroy(s->own);
