@@ -132,6 +132,7 @@ struct KParams {
     uint32_t s_magic;           // ceil(2^32 / s) for k / s by a multiply-high (s <= 1625), else 0
     uint32_t endgame;           // dry cursor and at most this many pixels unfinished: park at the
                                 // next sample boundary (0: off)
+    uint32_t probe_sub;         // cost probe on every probe_sub-th pixel of every probe_sub-th row
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -1304,12 +1305,19 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kBvh>(P, lds_sph);
     uint16_t *scol = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lds_sph) + P.lane_lds_off) + threadIdx.x;
-    const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
+    // probe_sub > 1: one probed pixel per probe_sub x probe_sub block stands for the
+    // block in its tile's cost (the others keep pcost 0: ordered with their tile)
+    const uint32_t sub = P.probe_sub > 1u ? P.probe_sub : 1u;
+    const uint32_t wq = (P.W + sub - 1u) / sub, hq = (P.n_rows + sub - 1u) / sub;
+    const uint64_t nq = static_cast<uint64_t>(wq) * hq;
     Tally tl;
     Stamps stp;
-    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < npix;
-         i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-        const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
+    for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < nq;
+         j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        const uint32_t qr = static_cast<uint32_t>(j / wq), qx = static_cast<uint32_t>(j - static_cast<uint64_t>(qr) * wq);
+        const uint32_t lr = qr * sub, x = qx * sub;
+        const uint64_t i = static_cast<uint64_t>(lr) * P.W + x;
+        const uint32_t wgt = min(sub, P.W - x) * min(sub, P.n_rows - lr);
         const PixelLoc pl(P, x, P.row_begin + lr * P.row_step);
         U128 rng = P.seeds[i];  // a copy: the render starts from the same child
         uint32_t segs = 0;
@@ -1329,7 +1337,7 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         P.pcost[i] = segs;
         const TileGrid tg(P);
         if (segs >= kHotSegs) atomicAdd(P.cost + tg.count() + tg.of(x, lr), 1u);
-        else atomicAdd(P.cost + tg.of(x, lr), segs);
+        else atomicAdd(P.cost + tg.of(x, lr), segs * wgt);
     }
 }
 // per tile: cost bucket of its non-hot pixels and their count into the histogram
@@ -2431,6 +2439,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
+            P.probe_sub = 1;
+            if (const char *e = std::getenv("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+            if (P.probe_sub > 1) HIPCHECK(hipMemsetAsync(s->d_pcost, 0, npix * sizeof(uint32_t), st));
             // probe: scene + per-lane walk stacks in LDS when they fit, one workgroup per CU
             KParams Q = P;
             Q.lane_lds_off = static_cast<uint32_t>((lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, true, P.n_nbr) + 15) & ~size_t(15));

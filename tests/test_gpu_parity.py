@@ -199,6 +199,7 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0.3", "join5"), ("2", "1.5", "join50"),  # priority waves join the cursor (RTW_JOIN %)
     ("2", "0", "endgame"), ("2", "0.3", "endgame"),  # dry cursor: park everything (RTW_ENDGAME)
     ("2", "0", "endgame_coopg16"),
+    ("2", "0", "probe2"), ("2", "0.3", "probe3"),  # cost probe on one pixel per 2x2 / 3x3 block
 ]
 
 
@@ -218,6 +219,7 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_JOIN", {"join5": "5", "join50": "50"}.get(coop, "0"))
     endgame = coop.startswith("endgame")
     monkeypatch.setenv("RTW_ENDGAME", "100000000" if endgame else "0")
+    monkeypatch.setenv("RTW_PROBE_SUB", coop[5:] if coop.startswith("probe") else "1")
     if coop == "endgame_coopg16":
         monkeypatch.setenv("RTW_COOPG", "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
