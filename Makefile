@@ -6,7 +6,9 @@ HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 # xnack- : the pool runs without XNACK (no page-fault retry), and code built for it is
 # free of the xnack-any constraints: 127.9 -> 127.5 ms per image, 8-round A/B
-# (profiles/r02_misc/ab_xnack_off.log)
+# (profiles/r02_misc/ab_xnack_off.log). Such a code object does not load on a gfx950
+# running with XNACK enabled: `make ARCH=gfx950` builds the portable (xnack-any) one.
+# rtw_version() names the target feature the library was built for.
 ARCH ?= gfx950:xnack-
 PKG := raytracing_in_a_weekend_rust_amd
 SRC := $(PKG)/csrc
@@ -15,6 +17,11 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-f
             -Wall -Iinclude -I$(SRC) -I$(SRC)/host $(EXTRA)
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
             -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
+# Build id: hash of every library source and the device flags. rtw_build_id()
+# returns it; profiles/ PMC files are stamped with it and bench.py refuses a file
+# whose stamp differs from the loaded library's.
+LIB_SRCS := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/host/*.cpp $(SRC)/host/*.h)) include/rtw_capi.h
+BUILD_ID := $(shell cat $(LIB_SRCS) | sha256sum | cut -c1-12)-$(shell echo '$(ARCH) $(HIPFLAGS)' | sha256sum | cut -c1-4)
 
 all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check
 
@@ -40,9 +47,17 @@ $(OUT)/next01_check: tools/next01_check.cpp $(SRC)/rtw_numeric.h
 $(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
 	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/accel_check.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
 
-$(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+# rewritten only when the id changes (so an unchanged tree rebuilds nothing)
+$(OUT)/rtw_build_id.h: FORCE
 	@mkdir -p $(OUT)
-	$(CXX) $(CXXFLAGS) -c $< -o $@
+	@echo '#define RTW_BUILD_ID "$(BUILD_ID)"' > $@.tmp
+	@echo '#define RTW_BUILD_ARCH "$(ARCH)"' >> $@.tmp
+	@cmp -s $@.tmp $@ || mv $@.tmp $@
+	@rm -f $@.tmp
+
+$(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h $(OUT)/rtw_build_id.h
+	@mkdir -p $(OUT)
+	$(CXX) $(CXXFLAGS) -I$(OUT) -c $< -o $@
 
 $(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
@@ -68,4 +83,5 @@ clean:
 	rm -rf $(OUT) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean stamps
+.PHONY: all oracle asm clean stamps FORCE
+FORCE:

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 5
+#define RTW_ABI_VERSION 6
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -104,12 +104,28 @@ typedef struct rtw_stats {
                                  no-progress guard ($RTW_SPIN_GUARD_MS, default 100)   */
     uint64_t leftover_pixels; /* parked pixels finished by the follow-up launch (after
                                  guard exits; 0 on an exclusive device)                 */
+    /* ABI 6: */
+    double main_kernel_ms;    /* the main render kernel alone (persistent / fast kernel),
+                                 HIP events around its launch; kernel_ms spans every
+                                 launch of the render (seeds, cost order, main, leftover) */
 } rtw_stats;
 
 /* ---- library ---- */
 const char *rtw_version(void);
+/* RTW_ABI_VERSION the library was built with. A client compares it with the
+ * RTW_ABI_VERSION of the header it was compiled against before passing any struct
+ * (rtw_stats grew in ABI 5 and ABI 6). */
+int rtw_abi_version(void);
+/* Hash of the library's sources and device flags (profiles/ counter files are
+ * stamped with it). */
+const char *rtw_build_id(void);
 const char *rtw_last_error(void);
 int rtw_device_count(int *count);
+/* Frees every device resource the library owns: the sessions behind
+ * rtw_threaded_render(_fast) and rtw_threaded_render_multi. Sessions the caller
+ * created with rtw_session_create stay the caller's. The next one-shot call
+ * re-creates what it needs. Not to be called while another thread renders. */
+int rtw_shutdown(void);
 
 /* ---- host mirror of the reference types (bit-exact f64, no FMA) ---- */
 /* Camera::new(img_height, img_width, max_depth, focal_length, fov, look_from,
@@ -164,6 +180,22 @@ int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32
                         const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
                         rtw_u128 seed, const rtw_shard *shard, double *out_rgb,
                         rtw_stats *stats);
+
+/* Camera::threaded_render on several GPUs of this node (camera.rs:223-227; the
+ * reference's pool takes every core, camera.rs:253 -- this takes every listed GPU).
+ * `devices` holds n_devices device indices; NULL or 0 = every visible device. An
+ * index may repeat: every entry gets its own session, stream and host thread.
+ * Rows are dealt cyclically -- image row r goes to entry r % n_devices (sky rows
+ * are cheap, ground rows are not) -- and each entry copies its rows straight into
+ * their places in out_rgb (host, H*W*3 f64) with one strided device-to-host copy:
+ * the gather needs no collective because the result is a host buffer. Pixels and
+ * their RNG streams depend only on the global pixel index, so the image is
+ * bit-identical to rtw_threaded_render's. stats (nullable): counters summed over
+ * the entries, kernel_ms = the slowest entry's render. */
+int rtw_threaded_render_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                              const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                              rtw_u128 seed, const int *devices, uint32_t n_devices, double *out_rgb,
+                              rtw_stats *stats);
 
 /* rtw_threaded_render in f32 fast mode (see rtw_session_render_fast). */
 int rtw_threaded_render_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,

@@ -4,7 +4,8 @@ Scene::hit / Sphere::hit -> Material::scatter), behind the C ABI in
 include/rtw_capi.h. See DESIGN.md."""
 from ._capi import LIB_PATH, RtwError  # noqa: F401  (raises ImportError if librtw.so is missing)
 from .api import (DEFAULT_SEED, Camera, Dielectric, Lambertian, Metal, Scene,  # noqa: F401
-                  SceneBuilder, Session, Sphere, builtin_scene, device_count, format_ppm,
-                  render_flat, render_flat_fast, seed_children, write_ppm, xorshift_next_01, xorshift_next_int)
+                  SceneBuilder, Session, Sphere, build_id, builtin_scene, device_count, format_ppm,
+                  render_flat, render_flat_fast, render_flat_multi, seed_children, shutdown, write_ppm,
+                  xorshift_next_01, xorshift_next_int)
 
-__version__ = "0.1.0"
+__version__ = "0.6.0"

@@ -73,7 +73,7 @@ class Stats(C.Structure):
                 ("brute_segments", C.c_uint64), ("accel", C.c_uint32), ("lds_bytes", C.c_uint32),
                 ("parked_pixels", C.c_uint64), ("inside_segments", C.c_uint64),
                 ("trap_segments", C.c_uint64), ("guard_exits", C.c_uint64),
-                ("leftover_pixels", C.c_uint64)]
+                ("leftover_pixels", C.c_uint64), ("main_kernel_ms", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -87,7 +87,10 @@ ERRORS = {-1: "RTW_E_ARG", -2: "RTW_E_EMPTY_IMAGE", -3: "RTW_E_FUZZ", -4: "RTW_E
 _P = C.POINTER
 SIGNATURES = {
     "rtw_version": (C.c_char_p, []),
+    "rtw_abi_version": (C.c_int, []),
+    "rtw_build_id": (C.c_char_p, []),
     "rtw_last_error": (C.c_char_p, []),
+    "rtw_shutdown": (C.c_int, []),
     "rtw_device_count": (C.c_int, [_P(C.c_int)]),
     "rtw_camera_new": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_double, C.c_double,
                                  _P(Vec3), _P(Vec3), _P(Vec3), C.c_double, C.c_double,
@@ -108,6 +111,9 @@ SIGNATURES = {
     "rtw_threaded_render": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                       C.c_uint32, C.c_uint32, U128, _P(Shard),
                                       _P(C.c_double), _P(Stats)]),
+    "rtw_threaded_render_multi": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
+                                            C.c_uint32, C.c_uint32, U128, _P(C.c_int), C.c_uint32,
+                                            _P(C.c_double), _P(Stats)]),
     "rtw_threaded_render_fast": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                            C.c_uint32, C.c_uint32, U128, _P(Shard),
                                            _P(C.c_float), _P(Stats)]),
@@ -157,6 +163,9 @@ def _load():
 
 
 lib = _load()
+ABI_VERSION = 6  # include/rtw_capi.h RTW_ABI_VERSION this binding's structs follow
+if lib.rtw_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH} has ABI {lib.rtw_abi_version()}, this binding expects {ABI_VERSION}")
 
 
 def check(rc: int) -> int:

@@ -197,6 +197,30 @@ def render_flat(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, seed=D
     return fb, st
 
 
+def render_flat_multi(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, seed=DEFAULT_SEED,
+                      devices=None):
+    """rtw_threaded_render_multi: the whole image over a list of GPUs (None = every
+    visible device; an index may repeat), rows dealt cyclically, gathered by strided
+    device-to-host copies into one host framebuffer. Returns (H x W x 3 f64, Stats)."""
+    fb = np.zeros((cam.img_height, cam.img_width, 3), dtype=np.float64)
+    st = capi.Stats()
+    devs = list(devices or [])
+    arr = (C.c_int * max(1, len(devs)))(*devs)
+    check(lib.rtw_threaded_render_multi(C.byref(cam), sph, n_sph, mats, n_mats, samples_sqrt,
+                                        capi.U128.of(seed), arr if devs else None, len(devs),
+                                        fb.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
+    return fb, st
+
+
+def shutdown():
+    """rtw_shutdown: frees the device resources of the one-shot and multi-GPU calls."""
+    check(lib.rtw_shutdown())
+
+
+def build_id() -> str:
+    return lib.rtw_build_id().decode()
+
+
 def render_flat_fast(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, seed=DEFAULT_SEED,
                      shard=None):
     """rtw_threaded_render_fast (f32 fast mode, statistical parity): host buffers in,

@@ -22,16 +22,30 @@ struct Config {  // main.rs:13-29
     uint32_t height = 1080, width = 1920, sample_sqrt = 10, depth = 0;
     bool preview = false;
     std::string scene = "complex", out = "img.ppm";
-    unsigned long long seed = 0;
+    unsigned __int128 seed = 0;
     bool seed_set = false;
     bool fast = false;
 };
 
+// Rust's str::parse::<usize>() (main.rs:37-39): an optional '+', then decimal
+// digits only (no whitespace, no sign '-', no base prefix).
+bool parse_dec(const char *s, unsigned __int128 max, unsigned __int128 &v) {
+    if (!s) return false;
+    if (*s == '+') ++s;
+    if (!*s) return false;
+    unsigned __int128 x = 0;
+    for (; *s; ++s) {
+        if (*s < '0' || *s > '9') return false;
+        const unsigned d = static_cast<unsigned>(*s - '0');
+        if (x > (max - d) / 10) return false;
+        x = x * 10 + d;
+    }
+    v = x;
+    return true;
+}
 bool parse_u32(const char *s, uint32_t &v) {
-    if (!s || !*s) return false;
-    char *end = nullptr;
-    const unsigned long long x = std::strtoull(s, &end, 10);
-    if (*end || s[0] == '-' || x > 0xffffffffull) return false;
+    unsigned __int128 x = 0;
+    if (!parse_dec(s, 0xffffffffu, x)) return false;
     v = static_cast<uint32_t>(x);
     return true;
 }
@@ -52,7 +66,13 @@ Config parse_args(int argc, char **argv) {
         else if (a == "--samplesqrt" || a == "-s") need(c.sample_sqrt, "--samplesqrt");
         else if (a == "--depth" || a == "-d") need(c.depth, "--depth");
         else if (a == "--preview" || a == "-p") c.preview = true;
-        else if (a == "--seed" && next) c.seed = std::strtoull(next, nullptr, 0), c.seed_set = true;
+        else if (a == "--seed") {  // decimal, up to 2^128 - 1 (XorShift state is a u128)
+            if (!parse_dec(next, ~static_cast<unsigned __int128>(0), c.seed)) {
+                std::fprintf(stderr, "Usage: --seed <decimal number>\n");
+                std::exit(1);
+            }
+            c.seed_set = true;
+        }
         else if (a == "--scene" && next) c.scene = next;
         else if (a == "--out" && next) c.out = next;
         else if (a == "--mode" && next) {
@@ -69,7 +89,7 @@ Config parse_args(int argc, char **argv) {
             std::printf("\t--samplesqrt -s\t:\tSet the sqrt of the samples used for the image\n");
             std::printf("\t--preview -p\t:\tSet whether a preview window is displayed (ignored)\n");
             std::printf("\t--depth -d\t:\tMax bounce depth (reference: 10)\n");
-            std::printf("\t--seed N\t:\tXorShift seed for scene and render (reference: wall-clock ms)\n");
+            std::printf("\t--seed N\t:\tXorShift seed (decimal) for scene and render (reference: wall-clock ms)\n");
             std::printf("\t--scene NAME\t:\tcomplex | simple | threads | super_simple | three_lambertian\n");
             std::printf("\t--out PATH\t:\tOutput PPM (reference: img.ppm)\n");
             std::printf("\t--mode M\t:\tparity (f64, bit-exact; default) | fast (f32, statistical)\n");
@@ -84,13 +104,22 @@ Config parse_args(int argc, char **argv) {
     return c;
 }
 
+std::string dec(unsigned __int128 v) {
+    std::string r;
+    do {
+        r.insert(r.begin(), static_cast<char>('0' + static_cast<int>(v % 10)));
+        v /= 10;
+    } while (v);
+    return r;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
     const Config cfg = parse_args(argc, argv);
     if (cfg.preview) std::fprintf(stderr, "note: --preview is not supported; rendering headless\n");
     try {
-        const rtw_u128 seed{cfg.seed, 0};
+        const rtw_u128 seed{static_cast<uint64_t>(cfg.seed), static_cast<uint64_t>(cfg.seed >> 64)};
         rtw::BuiltScene b = rtw::build_scene(cfg.scene, seed, cfg.height, cfg.width, cfg.depth);
         std::printf(
             "\n            Multithreaded rendering\n            Making an image of format:\n"
@@ -114,11 +143,12 @@ int main(int argc, char **argv) {
             rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st);
         }
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("Finished succesfully: %s (%.3f s wall, kernel %.3f ms, %.1f Msamples/s, seed %llu)\n",
-                    cfg.out.c_str(), s, st.kernel_ms, st.samples / st.kernel_ms / 1e3, cfg.seed);
+        std::printf("Finished succesfully: %s (%.3f s wall, kernel %.3f ms, %.1f Msamples/s, seed %s)\n",
+                    cfg.out.c_str(), s, st.kernel_ms, st.samples / st.kernel_ms / 1e3, dec(cfg.seed).c_str());
     } catch (const rtw::Error &e) {
+        // main.rs:106-110: the render thread's error is printed, and main still
+        // returns Ok(()) -- exit status 0, as the reference
         std::fprintf(stderr, "\nRender thread errored with %s\n", e.what());
-        return 1;
     }
     return 0;
 }

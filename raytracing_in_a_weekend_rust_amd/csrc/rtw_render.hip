@@ -28,8 +28,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <exception>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rtw_accel.h"
@@ -133,6 +136,8 @@ struct KParams {
     uint32_t endgame;           // dry cursor and at most this many pixels unfinished: park at the
                                 // next sample boundary (0: off)
     uint32_t probe_sub;         // cost probe on every probe_sub-th pixel of every probe_sub-th row
+    uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
+                                // pixel; the leftover launch finishes them all
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -1812,7 +1817,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint32_t sub = threadIdx.x & (kCoopG - 1u);
     const int gl = static_cast<int>(lane & ~(kCoopG - 1u));
     uint32_t cseg = 0;
-    for (;;) {
+    // RTW_DRAIN_OFF=1 (tests): no drain here, so every parked pixel is left to the
+    // follow-up launch (rtw_park_leftover) -- that path then runs on every entry
+    for (bool drain = !KP(drain_off); drain;) {
         uint32_t t = 0, state = 0;  // state 1: ticket t is published, 2: stop
         if (sub == 0) {
             t = atomicAdd(P.park_cursor, 1u);
@@ -2011,6 +2018,8 @@ struct rtw_session {
     unsigned long long *d_fcount = nullptr;
     bool last_fast = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;  // around the main kernel (rtw_stats.main_kernel_ms)
+    bool main_ev = false;                         // the last render recorded them
     uint32_t *d_err = nullptr;  // latched count of incomplete renders (rtw_latch_check)
     hipStream_t last_stream = nullptr;
     bool pending = false;
@@ -2522,10 +2531,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = std::getenv("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};
+        HIPCHECK(hipEventRecord(s->ev_k0, st));
         HIPCHECK(hipLaunchKernel(fn, dim3(grid_p), dim3(pblock), args, lds, st));
+        HIPCHECK(hipEventRecord(s->ev_k1, st));
         // entries no group claimed (only after guard exits); returns at once otherwise
         const size_t lds2 = lds_bytes_for(P.n_sph, 0, 0, false) + static_cast<size_t>(P.n_sph) * sizeof(float4);
         const dim3 grid_l(static_cast<uint32_t>(s->n_cu > 0 ? s->n_cu : 256));
@@ -2577,6 +2589,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     s->last.accel = static_cast<uint32_t>(mode);
     s->last.lds_bytes = static_cast<uint32_t>(lds);
     s->last_fast = false;
+    s->main_ev = P.n_rows && persist;
 }
 
 // f32 fast mode (rtw_fast.hip): same camera, shard and validation as render().
@@ -2635,7 +2648,9 @@ void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, r
     HIPCHECK(hipSetDevice(s->device));
     order_after_last(s, st);
     HIPCHECK(hipEventRecord(s->ev0, st));
+    HIPCHECK(hipEventRecord(s->ev_k0, st));
     HIPCHECK(rtw_fast::launch(F, s->n_cu, st));
+    HIPCHECK(hipEventRecord(s->ev_k1, st));
     hipLaunchKernelGGL(rtw_latch_check<unsigned long long>, dim3(1), dim3(64), 0, st,
                        static_cast<const unsigned long long *>(s->d_fcount + 2),
                        static_cast<unsigned long long>(F.n_rows) * F.W, s->d_err);
@@ -2653,6 +2668,7 @@ void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, r
     bool in_lds = false;
     s->last.lds_bytes = static_cast<uint32_t>(rtw_fast::lds_bytes(F.n_sph, F.n_node, F.n_stack, &in_lds));
     s->last_fast = true;
+    s->main_ev = true;
 }
 
 // Latched incomplete renders since the last check (rtw_latch_check): reported
@@ -2673,6 +2689,8 @@ void collect(rtw_session *s) {
     HIPCHECK(hipEventSynchronize(s->ev1));
     s->pending = false;
     check_latch(s);
+    float main_ms = 0.f;
+    if (s->main_ev) HIPCHECK(hipEventElapsedTime(&main_ms, s->ev_k0, s->ev_k1));
     if (s->last_fast) {
         unsigned long long c[5] = {};
         HIPCHECK(hipMemcpy(c, s->d_fcount, sizeof c, hipMemcpyDeviceToHost));
@@ -2684,6 +2702,7 @@ void collect(rtw_session *s) {
         s->last.exact_wave_iterations = c[4];  // fast mode: wave-level walk iterations (RTW_FAST_DIAG builds)
         s->last.sphere_tests = c[0] * s->n_sph;
         s->last.kernel_ms = ms;
+        s->last.main_kernel_ms = main_ms;
         if (c[2] != s->last.pixels)  // never a silently incomplete image
             throw rtw::Error(RTW_E_HIP, "fast render incomplete: " + std::to_string(c[2]) + " of " +
                                             std::to_string(s->last.pixels) + " pixels written");
@@ -2706,6 +2725,7 @@ void collect(rtw_session *s) {
     s->last.leftover_pixels = c[10];
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
+    s->last.main_kernel_ms = s->main_ev ? main_ms : ms;
     uint32_t ctl[8] = {};
     HIPCHECK(hipMemcpy(ctl, s->d_park_ctl, sizeof ctl, hipMemcpyDeviceToHost));
     if (ctl[4] != static_cast<uint32_t>(s->last.pixels))  // never a silently incomplete image
@@ -2729,6 +2749,8 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipStreamCreateWithFlags(&s->own, hipStreamNonBlocking));
         HIPCHECK(hipEventCreate(&s->ev0));
         HIPCHECK(hipEventCreate(&s->ev1));
+        HIPCHECK(hipEventCreate(&s->ev_k0));
+        HIPCHECK(hipEventCreate(&s->ev_k1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_err, sizeof(uint32_t)));
@@ -2759,36 +2781,123 @@ void create_session(int device, rtw_session **out) {
         return RTW_E_ARG;                     \
     }
 
-// Host-buffer render on a cached session of $RTW_DEVICE (the blocking
+// Sessions the library owns (rtw_shutdown frees them): the one-shot API's session
+// of $RTW_DEVICE, and one per entry of rtw_threaded_render_multi's device list.
+static std::mutex g_one_mu;
+static rtw_session *g_one = nullptr;
+static std::mutex g_multi_mu;
+static std::vector<rtw_session *> g_multi;
+
+// grow-only device framebuffer of a library-owned session
+static void *session_out(rtw_session *s, size_t bytes) {
+    bytes = std::max<size_t>(bytes, 8);
+    if (bytes > s->out_cap) {
+        dev_free(s->d_out);
+        s->d_out = nullptr, s->out_cap = 0;
+        HIPCHECK(hipMalloc(&s->d_out, bytes));
+        s->out_cap = bytes;
+    }
+    return s->d_out;
+}
+
+// Host-buffer render on the cached session of $RTW_DEVICE (the blocking
 // Camera::threaded_render shape): upload, enqueue `run`, wait, download.
 template <typename T, typename Run>
 int threaded(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres, const rtw_material *mats,
              uint32_t n_mats, const rtw_shard *shard, T *out_rgb, rtw_stats *stats, Run run) {
     if (!cam || !out_rgb) return rtw::set_error("null argument"), RTW_E_ARG;
-    static std::mutex mu;
-    static rtw_session *cached = nullptr;
-    std::lock_guard<std::mutex> lock(mu);
+    std::lock_guard<std::mutex> lock(g_one_mu);
     RTW_GUARD_BEGIN
     if (cam->img_height == 0 || cam->img_width == 0)
         throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
     validate_scene(spheres, n_spheres, mats, n_mats);
     const rtw_shard sh = resolve_shard(cam, shard);
     const int dev = default_device();
-    if (cached && cached->device != dev) rtw_session_destroy(cached), cached = nullptr;
-    if (!cached) create_session(dev, &cached);
-    set_scene(cached, spheres, n_spheres, mats, n_mats);
+    if (g_one && g_one->device != dev) rtw_session_destroy(g_one), g_one = nullptr;
+    if (!g_one) create_session(dev, &g_one);
+    set_scene(g_one, spheres, n_spheres, mats, n_mats);
     const size_t bytes = static_cast<size_t>(sh.n_rows) * cam->img_width * 3 * sizeof(T);
-    if (std::max<size_t>(bytes, 8) > cached->out_cap) {  // grow-only device framebuffer
-        dev_free(cached->d_out);
-        cached->d_out = nullptr, cached->out_cap = 0;
-        HIPCHECK(hipMalloc(&cached->d_out, std::max<size_t>(bytes, 8)));
-        cached->out_cap = std::max<size_t>(bytes, 8);
-    }
-    T *d_out = static_cast<T *>(cached->d_out);
-    run(cached, &sh, d_out, cached->own);
-    collect(cached);
+    T *d_out = static_cast<T *>(session_out(g_one, bytes));
+    run(g_one, &sh, d_out, g_one->own);
+    collect(g_one);
     if (bytes) HIPCHECK(hipMemcpy(out_rgb, d_out, bytes, hipMemcpyDeviceToHost));
-    if (stats) *stats = cached->last;
+    if (stats) *stats = g_one->last;
+    return RTW_OK;
+    RTW_GUARD_END
+}
+
+// Counters of several shards of one image: sums, the slowest render's time.
+static void add_stats(rtw_stats &a, const rtw_stats &b, bool first) {
+    if (first) {
+        a = b;
+        return;
+    }
+    a.pixels += b.pixels, a.samples += b.samples, a.segments += b.segments;
+    a.sphere_tests += b.sphere_tests, a.wave_iterations += b.wave_iterations;
+    a.exact_tests += b.exact_tests, a.exact_wave_iterations += b.exact_wave_iterations;
+    a.kernel_ms = std::max(a.kernel_ms, b.kernel_ms);
+    a.node_visits += b.node_visits, a.brute_segments += b.brute_segments;
+    a.parked_pixels += b.parked_pixels, a.inside_segments += b.inside_segments;
+    a.trap_segments += b.trap_segments, a.guard_exits += b.guard_exits;
+    a.leftover_pixels += b.leftover_pixels;
+}
+
+// rtw_threaded_render_multi: one host thread per device entry, rows r = i mod n.
+static int threaded_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres, const rtw_material *mats,
+                   uint32_t n_mats, uint32_t samples_sqrt, rtw_u128 seed, const int *devices, uint32_t n_devices,
+                   double *out_rgb, rtw_stats *stats) {
+    if (!cam || !out_rgb || (n_devices && !devices)) return rtw::set_error("null argument"), RTW_E_ARG;
+    std::lock_guard<std::mutex> lock(g_multi_mu);
+    RTW_GUARD_BEGIN
+    if (cam->img_height == 0 || cam->img_width == 0)
+        throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");
+    validate_scene(spheres, n_spheres, mats, n_mats);
+    int visible = 0;
+    if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) throw rtw::Error(RTW_E_NO_DEVICE, "no HIP device");
+    std::vector<int> devs;
+    if (n_devices == 0) {
+        for (int d = 0; d < visible; ++d) devs.push_back(d);
+    } else {
+        devs.assign(devices, devices + n_devices);
+    }
+    for (int d : devs)
+        if (d < 0 || d >= visible) throw rtw::Error(RTW_E_NO_DEVICE, "device index out of range");
+    const uint32_t H = cam->img_height, W = cam->img_width;
+    const uint32_t n = static_cast<uint32_t>(std::min<size_t>(devs.size(), H));  // extra entries: no rows
+    if (g_multi.size() < n) g_multi.resize(n, nullptr);
+    std::vector<std::thread> workers;
+    std::vector<std::exception_ptr> errs(n);
+    std::vector<rtw_stats> st(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        workers.emplace_back([&, i] {
+            try {
+                rtw_session *&s = g_multi[i];
+                if (s && s->device != devs[i]) rtw_session_destroy(s), s = nullptr;
+                if (!s) create_session(devs[i], &s);
+                HIPCHECK(hipSetDevice(s->device));
+                set_scene(s, spheres, n_spheres, mats, n_mats);
+                const rtw_shard sh{i, n, (H - i + n - 1) / n, 0};
+                const size_t row = static_cast<size_t>(W) * 3 * sizeof(double);
+                double *d_out = static_cast<double *>(session_out(s, sh.n_rows * row));
+                render(s, cam, samples_sqrt, seed, &sh, d_out, s->own);
+                collect(s);
+                // the gather: tile row k -> image row i + k n, one strided copy
+                HIPCHECK(hipMemcpy2D(out_rgb + static_cast<size_t>(i) * W * 3, n * row, d_out, row, row, sh.n_rows,
+                                     hipMemcpyDeviceToHost));
+                st[i] = s->last;
+            } catch (...) {
+                errs[i] = std::current_exception();
+            }
+        });
+    }
+    for (auto &w : workers) w.join();
+    for (auto &e : errs)
+        if (e) std::rethrow_exception(e);
+    if (stats) {
+        rtw_stats acc{};
+        for (uint32_t i = 0; i < n; ++i) add_stats(acc, st[i], i == 0);
+        *stats = acc;
+    }
     return RTW_OK;
     RTW_GUARD_END
 }
@@ -2823,6 +2932,8 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->ev_k0) (void)hipEventDestroy(s->ev_k0);
+    if (s->ev_k1) (void)hipEventDestroy(s->ev_k1);
     if (s->own) (void)hipStreamDestroy(s->own);
     delete s;
     return RTW_OK;
@@ -2884,6 +2995,24 @@ int rtw_threaded_render(const rtw_camera *cam, const rtw_sphere *spheres, uint32
                     [&](rtw_session *s, const rtw_shard *sh, double *d, hipStream_t st) {
                         render(s, cam, samples_sqrt, seed, sh, d, st);
                     });
+}
+
+int rtw_threaded_render_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                              const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                              rtw_u128 seed, const int *devices, uint32_t n_devices, double *out_rgb,
+                              rtw_stats *stats) {
+    return threaded_multi(cam, spheres, n_spheres, mats, n_mats, samples_sqrt, seed, devices, n_devices, out_rgb,
+                          stats);
+}
+
+int rtw_shutdown(void) {
+    std::lock_guard<std::mutex> l1(g_one_mu);
+    std::lock_guard<std::mutex> l2(g_multi_mu);
+    rtw_session_destroy(g_one);
+    g_one = nullptr;
+    for (auto *s : g_multi) rtw_session_destroy(s);
+    g_multi.clear();
+    return RTW_OK;
 }
 
 int rtw_threaded_render_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,

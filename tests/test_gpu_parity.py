@@ -428,6 +428,25 @@ def test_no_progress_guard_and_leftover_launch(monkeypatch, coop):
     print(f"guard exits {st.guard_exits}, leftover pixels {st.leftover_pixels}")
 
 
+@pytest.mark.parametrize("budget", ["0.01", "0.3"])
+def test_leftover_launch_finishes_every_parked_pixel(monkeypatch, budget):
+    """The persistent kernel with its drain switched off (RTW_DRAIN_OFF=1, no
+    priority waves): every parked pixel is published and left unclaimed, so the
+    follow-up launch (rtw_park_leftover) finishes all of them -- its region-B spill
+    columns by slot, the pass-1 records it stages and its published-flag filter.
+    Budget 0.01 parks every pixel after its first sample."""
+    monkeypatch.setenv("RTW_DRAIN_OFF", "1")
+    monkeypatch.setenv("RTW_HEAVY", "0")
+    monkeypatch.setenv("RTW_BUDGET_X", budget)
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
+    fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
+    ref, seg = oracle(cam, sph, n, mt, nm, 3, SEED)
+    assert_same(fb, ref, st, seg)
+    assert st.parked_pixels > 0 and st.leftover_pixels == st.parked_pixels
+    if budget == "0.01":
+        assert st.parked_pixels == 45 * 80
+
+
 def test_default_guard_leaves_nothing_behind():
     """On an exclusive device the default guard never fires: every parked pixel
     is finished inside the persistent kernel."""
@@ -457,3 +476,29 @@ def test_session_renders_on_two_streams_are_serialized():
     assert np.array_equal(b.cpu().numpy(), ref_b)
     assert st.pixels == 60 * 96
     sess.close()
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0], None])
+def test_multi_device_abi_matches_single_device(devices):
+    """rtw_threaded_render_multi (the multi-GPU Camera::threaded_render through the
+    C ABI alone): one session + host thread per entry, rows dealt cyclically,
+    gathered by strided device-to-host copies. Repeating device 0 exercises
+    several sessions and streams on the one GPU of the test box; None = every
+    visible device. Bit-exact against the single-device image."""
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 61, 96, 50)
+    ref, st = gpu(cam, sph, n, mt, nm, 3, SEED)
+    fb, mst = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 3, SEED, devices=devices)
+    assert np.array_equal(fb, ref)
+    assert mst.segments == st.segments and mst.pixels == 61 * 96 and mst.samples == st.samples
+
+
+def test_shutdown_frees_and_recreates_sessions():
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 30, 40, 50)
+    ref, _ = gpu(cam, sph, n, mt, nm, 2, SEED)
+    rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 2, SEED, devices=[0, 0])
+    rtw.shutdown()
+    fb, _ = gpu(cam, sph, n, mt, nm, 2, SEED)  # the one-shot session is re-created
+    assert np.array_equal(fb, ref)
+    fb, _ = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 2, SEED, devices=[0, 0, 0, 0])
+    assert np.array_equal(fb, ref)
+    rtw.shutdown()

@@ -214,3 +214,53 @@ def test_reference_asserts_become_error_codes():
     assert rc == -1
     assert capi.lib.rtw_threaded_render(None, sph, n, mt, nm, 2, capi.U128.of(1), None,
                                         fb.ctypes.data_as(P), None) == -1
+
+
+def test_abi_version_and_build_id():
+    assert capi.lib.rtw_abi_version() == capi.ABI_VERSION == 6
+    bid = rtw.build_id()
+    assert re.fullmatch(r"[0-9a-f]{12}-[0-9a-f]{4}", bid), bid
+    assert bid.encode() in capi.lib.rtw_version()
+
+
+def test_multi_device_render_validates_before_touching_a_device():
+    """rtw_threaded_render_multi mirrors the reference's asserts (camera.rs:267,
+    materials.rs:47) before any device work, and rtw_shutdown is always safe."""
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", rtw.DEFAULT_SEED, 9, 16, 10)
+    out = np.zeros((9, 16, 3))
+    P = C.POINTER(C.c_double)
+    empty = capi.Camera.from_buffer_copy(cam.raw)
+    empty.img_width = 0
+    rc = capi.lib.rtw_threaded_render_multi(C.byref(empty), sph, n, mt, nm, 2, capi.U128.of(1), None, 0,
+                                            out.ctypes.data_as(P), None)
+    assert rc == -2  # RTW_E_EMPTY_IMAGE
+    bad = (capi.Material * nm)(*mt[:nm])
+    for i in range(nm):
+        if bad[i].kind == capi.METAL:
+            bad[i].fuzz = 1.5
+            break
+    rc = capi.lib.rtw_threaded_render_multi(C.byref(cam.raw), sph, n, bad, nm, 2, capi.U128.of(1), None, 0,
+                                            out.ctypes.data_as(P), None)
+    assert rc == -3  # RTW_E_FUZZ
+    rc = capi.lib.rtw_threaded_render_multi(C.byref(cam.raw), sph, n, mt, nm, 2, capi.U128.of(1), None, 2,
+                                            out.ctypes.data_as(P), None)
+    assert rc == -1  # n_devices without a list
+    assert capi.lib.rtw_shutdown() == 0
+    assert capi.lib.rtw_shutdown() == 0
+
+
+def test_cli_argument_parsing_mirrors_main_rs(tmp_path):
+    """rtw_cli parses numbers as Rust's str::parse (decimal, optional '+'; main.rs:
+    37-39), exits 1 with a usage line on a bad number, and -- as main.rs:106-122 --
+    reports a render error on stderr yet exits 0."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(capi.LIB_PATH), "rtw_cli")
+    out = str(tmp_path / "img.ppm")
+    for bad in (["--seed", "0x10"], ["--seed", "-3"], ["-h", "12a"], ["--width", ""], ["-s"]):
+        r = subprocess.run([cli, *bad, "--out", out], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 1 and "Usage" in r.stderr, (bad, r.stderr)
+    env = dict(os.environ, RTW_DEVICE="9999")  # no such device: the render errors
+    r = subprocess.run([cli, "--seed", "010", "-h", "+4", "-w", "4", "-s", "1", "--out", out],
+                       capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0 and "Render thread errored" in r.stderr, r.stderr
+    assert "seed 10)" not in r.stdout  # nothing rendered
