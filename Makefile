@@ -79,9 +79,13 @@ asm: $(SRC)/rtw_render.hip
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/rtw_render.s $<
 
+# A/B variant of the library (tools/libab.py): make ablib NAME=x EXTRA=-DFOO -> ab/x/librtw.so
+ablib:
+	$(MAKE) OUT=ab/$(NAME) EXTRA='$(EXTRA)' ab/$(NAME)/librtw.so
+
 clean:
 	rm -rf $(OUT) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean stamps FORCE
+.PHONY: all oracle asm clean stamps ablib FORCE
 FORCE:

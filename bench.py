@@ -6,55 +6,69 @@ scene (raytracing::complex, raytracing/mod.rs:54-126; 486 spheres at the fixed
 scene seed), 1200x675, spp=500 -> samples_sqrt 23 (529 spp, the reference API
 takes samples_sqrt), max_depth 50, f64 parity mode (bit-identical to the
 reference restatement). One step = one whole-image render (Camera::threaded_render
-equivalent) with the scene already resident in HBM.
+equivalent, camera.rs:223-352) with the scene already resident in HBM.
+`--size WxH --samples-sqrt S --depth D` select the other BASELINE configs
+(config 3: --samples-sqrt 10; a config-5 rank: --size 4096x2304 --samples-sqrt 45
+under torchrun --nproc-per-node 8).
 
-N>1 (one rank per GPU): by default weak scaling -- the job renders N frames, rank r
-frame r (render seed SEED + r, shard.frame_seed), each a full 1200x675 spp-529
-image, with no data-path collective (frames are independent).
-`--scaling strong` renders the ONE frame row-cyclically sharded over the ranks and
-gathered over RCCL (all_gather of the row tiles) inside the timed step: BASELINE
-configs[3]'s scaling curve, whose per-rank times the serial per-pixel RNG chains
-bound.
+N>1 (one rank per GPU, BASELINE configs[3]'s scaling curve): by default the ONE
+frame is sharded row-cyclically over the ranks (row r -> rank r % N) and gathered
+over RCCL (all_gather of the padded row tiles + un-permute) inside the timed step;
+`--scaling weak` renders one whole frame per rank instead (render seed SEED + rank,
+no collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size WxH] [--samples-sqrt S]
+                    [--depth D] [--scaling strong|weak] [--mode parity|fast]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Rank 0 prints one JSON line (contract in the task statement). The cpu_baseline
-leg times the C oracle (test infrastructure, kind "port") on a bounded row
-sample of the same workload on this host, at N=1 only.
+Rank 0 prints one JSON line (contract in the task statement). After the timed
+region (N=1): the frame is hashed against the committed full-frame oracle
+fixture when one exists (`parity`), the render kernel's counters are collected by
+separate rocprofv3 --pmc passes of a one-frame child run (`roofline.valu_issue`,
+`roofline.traffic`), the one-shot ABI call with host buffers + PPM is timed
+(`end_to_end`), and the cpu_baseline leg times the C oracle (test infrastructure,
+kind "port") on a bounded row sample of the same workload.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
+import hashlib
 import json
 import os
+import re
+import shutil
+import signal
+import subprocess
 import sys
+import tempfile
 import time
-
-import torch  # first: librtw then shares torch's HIP runtime (same soname)
-import torch.distributed as dist
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-import raytracing_in_a_weekend_rust_amd as rtw  # noqa: E402
-from raytracing_in_a_weekend_rust_amd import shard  # noqa: E402
-
-SEED = rtw.DEFAULT_SEED
-W, H, SQRT, DEPTH = 1200, 675, 23, 50
+SEED = 1764892800000  # the package's DEFAULT_SEED (scene and render seed)
 FLOP_PER_TEST = 17  # SURVEY.md 8(d): oc 3, half_b 5, c 6 (r*r hoisted), disc 3
 FLOP_PER_VISIT = 20  # BVH walk step: slab test 6 FMA + 10 min/max, or the 17-FLOP sphere filter
 FP32_VECTOR_PEAK = 157.3  # TFLOP/s, MI355X spec (MI355X_MICROARCH.md chip table)
 FP64_VECTOR_PEAK = 78.6   # TFLOP/s, MI355X spec (SURVEY.md 8(d))
-PMC_FILE = os.path.join(HERE, "profiles", "pmc_traffic.json")
-INSTS_FILE = os.path.join(HERE, "profiles", "pmc_insts.json")
-GPU_CLOCK_HZ = 2.4e9  # MI355X peak engine clock (MI355X_MICROARCH.md)
-# gfx950 VALU issue (MI355X_MICROARCH.md cycle constants): a wave64 f32/int VALU
-# instruction occupies the 32-lane SIMD for 2 cycles; f64 FMA/MUL/ADD run at half
-# rate (4 cycles: FP64 vector peak = 1/2 FP32); one wave alone issues at most one
-# VALU instruction per 4 cycles.
-VALU_CYCLES = 2
-VALU_CYCLES_F64 = 4
+HBM_PEAK = 8000.0         # GB/s (MI355X_MICROARCH.md)
+GPU_CLOCK_HZ = 2.4e9      # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMD_LANES = 32           # a SIMD issues 32 lanes per cycle: a wave64 f32/int op takes 2 cycles
+MAIN_KERNEL = {"parity": "rtw_render_persist", "fast": "rtw_fast_render"}
+PMC_FALLBACK = os.path.join(HERE, "profiles", "r03_pmc.json")  # stamped with the build id
+# counter passes (never combined with tracing; FETCH_SIZE and WRITE_SIZE never share
+# a pass: MI355X_MICROARCH.md, rocprofv3 block limits)
+PMC_PASSES = {
+    "fetch": ["FETCH_SIZE"],
+    "write": ["WRITE_SIZE"],
+    "insts": ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VALU_TRANS_F64",
+              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
+              "SQ_INSTS_VALU_INT64"],
+    "cycles": ["SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU",
+               "SQ_ACTIVE_INST_ANY"],
+}
 
 
 def parse():
@@ -62,22 +76,132 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--samples-sqrt", type=int, default=SQRT)
-    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
-                   help="N>1: weak = one whole frame per rank (seed SEED+rank), no collective; "
-                        "strong = the one frame row-cyclically sharded + RCCL all_gather")
+    p.add_argument("--size", default="1200x675", help="WxH")
+    p.add_argument("--samples-sqrt", type=int, default=23)
+    p.add_argument("--depth", type=int, default=50)
+    p.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                   help="N>1: strong = the one frame row-cyclically sharded + RCCL all_gather "
+                        "(BASELINE configs[3]); weak = one whole frame per rank (seed SEED+rank)")
     p.add_argument("--mode", choices=("parity", "fast"), default="parity",
                    help="parity = f64 bit-exact (the headline); fast = the f32 mode with "
                         "independent per-sample streams (statistical parity, tests/test_gpu_fast.py)")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 disables the CPU leg")
     p.add_argument("--e2e", type=int, default=1,
                    help="0 disables the end-to-end leg (one-shot ABI call with host buffers + PPM)")
+    p.add_argument("--pmc", type=int, default=1,
+                   help="1: rocprofv3 --pmc passes of a one-frame child run (N=1, after the timed "
+                        "region); 0: only the build-stamped profiles/r03_pmc.json")
     p.add_argument("--cpu-row-stride", type=int, default=0,
                    help="oracle renders every k-th row (0 = auto, ~10-30 s)")
-    return p.parse_args()
+    p.add_argument("--pmc-out", default="",
+                   help="also write the live PMC summary (stamped with the build id) to this JSON file")
+    p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    a = p.parse_args()
+    a.width, a.height = (int(v) for v in a.size.lower().split("x"))
+    return a
 
 
-def end_to_end(cam, sph, ns, mt, nm, s, seed, fast, kernel_ms):
+def workload_name(a):
+    return f"complex_{a.width}x{a.height}_s{a.samples_sqrt}_d{a.depth}"
+
+
+# ----------------------------------------------------------------- PMC leg --
+def pmc_child(a):
+    """One frame of the workload through the one-shot ABI (the same launches as a
+    bench step), run under rocprofv3 --pmc by pmc_live()."""
+    import raytracing_in_a_weekend_rust_amd as rtw
+    cam, sph, ns, mt, nm = rtw.builtin_scene("complex", SEED, a.height, a.width, a.depth)
+    one_shot = rtw.render_flat_fast if a.mode == "fast" else rtw.render_flat
+    one_shot(cam.raw, sph, ns, mt, nm, a.samples_sqrt, SEED)
+
+
+def profiler_active():
+    pre = os.environ.get("LD_PRELOAD", "") + os.environ.get("HSA_TOOLS_LIB", "")
+    return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def read_counters(d):
+    """{kernel short name: {counter: per-dispatch mean}} from a rocprofv3 csv dir."""
+    acc, disp = {}, {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                m = re.search(r"\b((?:rtw|probe)_\w+)", row["Kernel_Name"])
+                short = m.group(1) if m else row["Kernel_Name"]
+                c = row["Counter_Name"]
+                k = (short, c)
+                acc[k] = acc.get(k, 0.0) + float(row["Counter_Value"])
+                disp.setdefault(k, set()).add(row.get("Dispatch_Id", row.get("Correlation_Id", "")))
+    out = {}
+    for (short, c), v in acc.items():
+        out.setdefault(short, {})[c] = v / max(1, len(disp[(short, c)]))
+    return out
+
+
+def pmc_live(a, timeout_s=150):
+    """Separate rocprofv3 --pmc passes over a one-frame child (no tracing in the same
+    run). Returns {pass: {kernel: {counter: value per dispatch}}} or None."""
+    exe = shutil.which("rocprofv3")
+    if not exe or profiler_active():
+        return None, "rocprofv3 not available" if not exe else "already under a profiler"
+    tmp = tempfile.mkdtemp(prefix="rtw_pmc_")
+    env = dict(os.environ, RTW_NO_TORCH="1", TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    res = {}
+    try:
+        for name, counters in PMC_PASSES.items():
+            d = os.path.join(tmp, name)
+            cmd = [exe, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--size", a.size,
+                   "--samples-sqrt", str(a.samples_sqrt), "--depth", str(a.depth), "--mode", a.mode]
+            p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
+                                 start_new_session=True, cwd=HERE)
+            try:
+                _, err = p.communicate(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.communicate()
+                return (res or None), f"pass {name} timed out"
+            if p.returncode != 0:
+                return (res or None), f"pass {name} exited {p.returncode}: {err.decode()[-300:]}"
+            res[name] = read_counters(d)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    return res, "live"
+
+
+def pmc_summary(res, kernel, build_id):
+    """Per-launch values of the main kernel (+ write bytes of every kernel of the render)."""
+    out = {"build_id": build_id, "kernel": kernel}
+    k = lambda p: (res.get(p) or {}).get(kernel, {})  # noqa: E731
+    if "FETCH_SIZE" in k("fetch") and "WRITE_SIZE" in k("write"):
+        # FETCH_SIZE x2: gfx950 counts half of a wide streaming read (MI355X_MICROARCH.md
+        # HBM section); both counters are in KB
+        out["fetch_bytes"] = 2.0 * 1024.0 * k("fetch")["FETCH_SIZE"]
+        out["write_bytes"] = 1024.0 * k("write")["WRITE_SIZE"]
+        out["write_bytes_by_kernel"] = {kn: round(1024.0 * v["WRITE_SIZE"])
+                                        for kn, v in res["write"].items() if "WRITE_SIZE" in v}
+    for c, v in k("insts").items():
+        out[c.lower()] = v
+    for c, v in k("cycles").items():
+        out[c.lower()] = v
+    return out
+
+
+def pmc_fallback(kernel, build_id):
+    try:
+        with open(PMC_FALLBACK) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, "no profiles/r03_pmc.json"
+    if d.get("kernel") != kernel or d.get("workload") != "complex_1200x675_s23_d50":
+        return None, "profiles/r03_pmc.json is for another kernel/workload"
+    if d.get("build_id") != build_id:
+        return None, f"profiles/r03_pmc.json is from build {d.get('build_id')}, library is {build_id}: refused"
+    return d, "profiles/r03_pmc.json (same build id)"
+
+
+# ------------------------------------------------------------ other legs --
+def end_to_end(rtw, cam, sph, ns, mt, nm, s, seed, fast, kernel_ms, npix):
     """SURVEY.md 8(d)'s end-to-end figure, outside the timed region: the one-shot
     rtw_threaded_render(_fast) (scene upload, seeds, render, framebuffer download to a
     host buffer: the reference's Camera::threaded_render, camera.rs:223-352) and then
@@ -91,7 +215,7 @@ def end_to_end(cam, sph, ns, mt, nm, s, seed, fast, kernel_ms):
     ppm = rtw.format_ppm(fb)
     t2 = time.perf_counter()
     render_ms, ppm_ms = (t1 - t0) * 1e3, (t2 - t1) * 1e3
-    samples = W * H * (s * s if s else 1)
+    samples = npix * (s * s if s else 1)
     return {"render_ms": round(render_ms, 3), "ppm_ms": round(ppm_ms, 3), "ppm_bytes": len(ppm),
             "host_overhead_ms": round(render_ms - kernel_ms, 3),
             "value": round(samples / ((render_ms + ppm_ms) / 1e3) / 1e6, 3), "unit": "Msamples/s",
@@ -138,79 +262,148 @@ def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
     threads, how = available_parallelism()
     if os.environ.get("RTW_CPU_THREADS"):
         threads, how = int(os.environ["RTW_CPU_THREADS"]), "RTW_CPU_THREADS override"
-    if stride <= 0:  # ~4 rows per thread: ~15 s of CPU work at ~0.16 Msamples/s/core
-        stride = max(1, int(round(cam.img_height / (4 * threads))))
+    if stride <= 0:  # ~4 rows per thread at the headline spp: ~15 s of CPU work
+        work = cam.img_width * (s * s if s else 1) / (1200 * 529)
+        stride = max(1, int(round(cam.img_height * work / (4 * threads))))
     n_rows = len(range(0, cam.img_height, stride))
     t0 = time.perf_counter()
-    _, seg = orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows),
-                        nthreads=threads, scheduler=0)
+    orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows), nthreads=threads, scheduler=0)
     dt = time.perf_counter() - t0
     samples = n_rows * cam.img_width * (s * s if s else 1)
     # also the "clean" scheduler (rows pulled by the workers, direct
     # calls, no per-pixel job/refcount overhead), on the same sampled rows
-    c_stride = stride
-    c_rows = len(range(0, cam.img_height, c_stride))
     t0 = time.perf_counter()
-    orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, c_stride, c_rows), nthreads=threads, scheduler=1)
+    orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows), nthreads=threads, scheduler=1)
     c_dt = time.perf_counter() - t0
-    c_samples = c_rows * cam.img_width * (s * s if s else 1)
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"rows 0::{stride} ({n_rows} rows x {cam.img_width} px x {s * s} spp, "
                       f"{samples / 1e6:.1f} Msamples) of the same image, {dt:.1f} s, "
                       f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible",
             "threads_rule": how,
-            "clean_scheduler": {"value": c_samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
-                                "sample": f"rows 0::{c_stride} ({c_rows} rows), {c_dt:.1f} s, row jobs, "
+            "clean_scheduler": {"value": samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
+                                "sample": f"rows 0::{stride} ({n_rows} rows), {c_dt:.1f} s, row jobs, "
                                           "direct calls"}}
+
+
+def parity_check(a, image, segments):
+    """The timed frame against the committed full-frame oracle fixture
+    (tests/golden/make_fullframe.py), outside the timed region."""
+    path = os.path.join(HERE, "tests", "golden", f"fullframe_{workload_name(a)}.json")
+    if a.mode != "parity" or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        fix = json.load(f)
+    fb = image.contiguous().cpu().numpy().astype("<f8", copy=False)
+    ok = hashlib.sha256(fb.tobytes()).hexdigest() == fix["fb_sha256"]
+    return {"fixture": os.path.relpath(path, HERE), "fb_sha256_ok": ok,
+            "segments_ok": segments == fix["segments"], "segments": segments,
+            "note": "last timed frame (gathered on rank 0 at N>1) vs the C oracle's full frame"}
+
+
+# ---------------------------------------------------------------- roofline --
+def roofline(a, st, kms, main_ms, pm, pm_source, n_cu, grid):
+    fast = a.mode == "fast"
+    t = main_ms / 1e3
+    brute_flop = st.sphere_tests * FLOP_PER_TEST
+    if st.accel == 2:
+        exec_flop = st.node_visits * FLOP_PER_VISIT + st.exact_tests * FLOP_PER_TEST
+    else:
+        exec_flop = brute_flop
+    npix = st.pixels
+    # SURVEY.md 8(d) algorithmic bytes: the framebuffer (24 B f64 / 12 B f32 a pixel)
+    # + the scene staged once per workgroup (n_spheres x 32 B)
+    alg_bytes = npix * (12 if fast else 24) + grid * st.sphere_tests // max(1, st.segments) * 32
+    simds = 4 * n_cu
+    peak_slots = simds * SIMD_LANES * GPU_CLOCK_HZ / 1e12  # T lane-slots/s (= 78.6 at 256 CUs)
+    r = {"bound": "valu", "achieved": None, "peak": round(peak_slots, 2),
+         "unit": "T VALU lane-slots/s", "frac": None, "traffic": None,
+         "kernel": MAIN_KERNEL[a.mode], "kernel_ms": round(main_ms, 3),
+         "render_ms": round(kms, 3),
+         "algorithmic_bytes_per_launch": alg_bytes,
+         "executed_flop_per_launch": exec_flop,
+         "executed_tflops": round(exec_flop / t / 1e12, 3),
+         "executed_frac_of_fp64_peak": round(exec_flop / t / 1e12 / FP64_VECTOR_PEAK, 4),
+         "executed_frac_of_fp32_peak": round(exec_flop / t / 1e12 / FP32_VECTOR_PEAK, 4),
+         "effective_bruteforce_tflops": round(brute_flop / t / 1e12, 3),
+         "bruteforce_flop_per_launch": brute_flop,
+         "pmc_source": pm_source,
+         "note": "frac = VALU issue: lane-slots the main kernel's VALU instructions occupy "
+                 "(PMC SQ_INSTS_VALU: 64 per wave64 f32/int op = 2 cycles of a 32-lane SIMD, "
+                 "128 per f64 op = 4 cycles) / (SIMDs x 32 lanes x 2.4 GHz x kernel_ms). "
+                 "executed_* = the work the BVH path runs (walk visits x 20 + exact f64 tests x "
+                 "17 FLOP); effective_bruteforce_tflops = the reference's brute-force Scene::hit "
+                 "work (segments x n_spheres x 17) over the same time, which the BVH does not "
+                 "execute (SURVEY 8(f) row 4: reported apart). traffic = HBM bytes per launch "
+                 "(PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes)."}
+    if pm and "sq_insts_valu" in pm:
+        n_valu = pm["sq_insts_valu"]
+        n_f64 = sum(pm.get(c, 0.) for c in ("sq_insts_valu_fma_f64", "sq_insts_valu_mul_f64",
+                                            "sq_insts_valu_add_f64", "sq_insts_valu_trans_f64"))
+        slots = 64.0 * (n_valu - n_f64) + 128.0 * n_f64
+        ach = slots / t / 1e12
+        r["achieved"] = round(ach, 3)
+        r["frac"] = round(ach / peak_slots, 4)
+        r["valu_issue"] = {"valu_insts_per_launch": n_valu, "f64_insts_per_launch": n_f64,
+                           "salu_insts_per_launch": pm.get("sq_insts_salu"),
+                           "lds_insts_per_launch": pm.get("sq_insts_lds"),
+                           "valu_insts_per_wave_segment": round(n_valu / max(1, st.segments / 64), 1)}
+        if pm.get("sq_wave_cycles"):
+            r["valu_issue"]["wait_any_share"] = round(pm.get("sq_wait_any", 0.) / pm["sq_wave_cycles"], 4)
+    if pm and "fetch_bytes" in pm:
+        tr = pm["fetch_bytes"] + pm["write_bytes"]
+        r["traffic"] = round(tr)
+        r["traffic_detail"] = {"fetch_bytes": round(pm["fetch_bytes"]), "write_bytes": round(pm["write_bytes"]),
+                               "traffic_over_algorithmic": round(tr / max(1, alg_bytes), 2),
+                               "hbm_gbps": round(tr / t / 1e9, 2), "hbm_frac": round(tr / t / 1e9 / HBM_PEAK, 6),
+                               "write_bytes_by_kernel": pm.get("write_bytes_by_kernel")}
+    return r
 
 
 def main():
     a = parse()
+    if a.pmc_child:
+        pmc_child(a)
+        return
+    import torch  # first: librtw then shares torch's HIP runtime (same soname)
+    import torch.distributed as dist
+
+    import raytracing_in_a_weekend_rust_amd as rtw
+    from raytracing_in_a_weekend_rust_amd import shard
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one rank per GPU)")
+    if world != a.gpus and world == 1 and a.gpus > 1:
+        raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one rank per GPU)")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    s = a.samples_sqrt
+    W, H, s, DEPTH = a.width, a.height, a.samples_sqrt, a.depth
     cam, sph, ns, mt, nm = rtw.builtin_scene("complex", SEED, H, W, DEPTH)
     n_off = s * s if s else 1
     weak = a.scaling == "weak"
-    if weak:  # frame `rank` of an N-frame job, the whole image on this rank
-        rb, rstep, rows_local, rm = 0, 1, H, H
-        render_seed = shard.frame_seed(SEED, rank)
-    else:  # row-cyclic shard of the one frame
-        rb, rstep, rows_local = shard.rows_of(rank, world, H)
-        rm = shard.rows_max(world, H)
-        render_seed = SEED
-    sess = rtw.Session(local)
-    sess.set_scene(sph, ns, mt, nm)
     dev = torch.device("cuda", local)
     fast = a.mode == "fast"
     fdt = torch.float32 if fast else torch.float64
-    fb = torch.zeros((rm, W, 3), dtype=fdt, device=dev)  # padded tile
+    sess = rtw.Session(local)
+    sess.set_scene(sph, ns, mt, nm)
+    plan = shard.StepPlan(world, rank, H, W, weak, SEED, fdt, dev)
     render = sess.render_fast if fast else sess.render
-    if world > 1 and not weak:
-        gathered = torch.empty((world * rm, W, 3), dtype=fdt, device=dev)
-        image = torch.empty((H, W, 3), dtype=fdt, device=dev)
-        index = shard.unpermute_index(world, H, dev)
     stream = torch.cuda.current_stream(dev)
     kernel_ms = []
+
+    def render_tile(pl):
+        render(cam.raw, s, pl.render_seed, pl.tile.data_ptr(), stream=stream.cuda_stream, shard=pl.shard)
 
     def step(record):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record(stream)
-        render(cam.raw, s, render_seed, fb.data_ptr(), stream=stream.cuda_stream,
-               shard=(rb, rstep, rows_local))
-        ev1.record(stream)
-        if world > 1 and not weak:  # RCCL all_gather of the row tiles + un-permute
-            shard.gather_image(fb, world, H, gathered, image, index)
+        # the rank's rows, then (N>1 strong) the RCCL all_gather of the row tiles +
+        # un-permute (SURVEY.md 8(e)); ev1 between them brackets the render alone
+        shard.step(plan, render_tile, after_render=lambda: ev1.record(stream))
         if record:
             kernel_ms.append((ev0, ev1))
 
@@ -228,64 +421,39 @@ def main():
     elapsed = time.perf_counter() - t0
     st = sess.stats()  # last render: deterministic counters of this rank's shard
     kms = sum(e0.elapsed_time(e1) for e0, e1 in kernel_ms) / max(1, len(kernel_ms))
+    segments = st.segments
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        sg = torch.tensor([segments], dtype=torch.int64, device=dev)
+        dist.all_reduce(sg, op=dist.ReduceOp.SUM)
+        segments = int(sg.item()) if not weak else st.segments
 
     frames = world if weak else 1
     total_samples = frames * W * H * n_off * a.steps
     value = total_samples / elapsed / 1e6
-    # `achieved` = SURVEY 8(d)'s algorithmic work: segments x N spheres x 17 FLOP (the
-    # reference's f64 brute-force Scene::hit) per launch over the kernel time. The
-    # exact BVH does not execute it: its executed work (walk visits ~20 FLOP each,
-    # f32, + exact f64 sphere tests 17 each) is reported beside it
-    brute_flop = st.sphere_tests * FLOP_PER_TEST
-    if st.accel == 2:
-        exec_flop = st.node_visits * FLOP_PER_VISIT + st.exact_tests * FLOP_PER_TEST
-    else:
-        exec_flop = brute_flop
-    achieved = brute_flop / (kms / 1e3) / 1e12
-    peak = FP32_VECTOR_PEAK if fast else FP64_VECTOR_PEAK
-    executed = exec_flop / (kms / 1e3) / 1e12
-    valu = None  # VALU issue utilisation from the committed PMC pass (profiles/pmc_insts.json)
-    if os.path.exists(INSTS_FILE) and world == 1 and not fast:
-        try:
-            with open(INSTS_FILE) as f:
-                pi = json.load(f)
-            if pi.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}":
-                n_valu = pi["sq_insts_valu_per_launch"]
-                n_f64 = sum(pi.get(k, 0.) for k in ("sq_insts_valu_fma_f64_per_launch",
-                                                    "sq_insts_valu_mul_f64_per_launch",
-                                                    "sq_insts_valu_add_f64_per_launch",
-                                                    "sq_insts_valu_trans_f64_per_launch"))
-                simds = 4 * torch.cuda.get_device_properties(0).multi_processor_count
-                # SIMD cycles the launch's VALU instructions occupy, over the SIMD-cycles available
-                busy = VALU_CYCLES * (n_valu - n_f64) + VALU_CYCLES_F64 * n_f64
-                avail = simds * GPU_CLOCK_HZ * (kms / 1e3)
-                valu = {"insts_per_launch": n_valu, "f64_insts_per_launch": n_f64,
-                        "achieved": round(n_valu / (kms / 1e3) / 1e9, 2),
-                        "unit": "G wave-instr/s", "simd_busy_frac": round(busy / avail, 3),
-                        "per_wave_segment": round(n_valu / max(1, st.segments / 64), 1),
-                        "note": "simd_busy_frac = (2 cyc x f32/int + 4 cyc x f64 VALU instructions, PMC "
-                                "SQ_INSTS_VALU*) / (SIMDs x clock x kernel time); profiles/pmc_insts.json "
-                                "is from the profiled build"}
-        except Exception:
-            valu = None
-    traffic = None
-    if os.path.exists(PMC_FILE):
-        try:
-            with open(PMC_FILE) as f:
-                pm = json.load(f)
-            if pm.get("workload") == f"complex_{W}x{H}_s{s}_d{DEPTH}" and world == 1 and not fast:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    parity = parity_check(a, plan.image, segments) if rank == 0 else None
 
     out = None
     if rank == 0:
+        pm, pm_source = None, "not collected (N>1)"
+        n_cu = torch.cuda.get_device_properties(local).multi_processor_count
+        if world == 1:
+            if a.pmc:
+                res, why = pmc_live(a)
+                if res and "insts" in res:
+                    pm, pm_source = pmc_summary(res, MAIN_KERNEL[a.mode], rtw.build_id()), "live rocprofv3 --pmc passes of a one-frame child run (this bench)"
+                    if a.pmc_out:
+                        with open(a.pmc_out, "w") as f:
+                            json.dump({**pm, "workload": workload_name(a), "mode": a.mode}, f, indent=1)
+                else:
+                    pm_source = f"live PMC failed ({why})"
+            if pm is None and a.mode == "parity" and workload_name(a) == "complex_1200x675_s23_d50":
+                pm, fb_why = pmc_fallback(MAIN_KERNEL[a.mode], rtw.build_id())
+                pm_source = (pm_source + "; " if a.pmc else "") + fb_why
         out = {
-            "metric": "Msamples/sec (pixels\u00d7spp) on final-scene 1200\u00d7675 spp=500 d=50; CPU-ref speedup",
+            "metric": "Msamples/sec (pixels×spp) on final-scene 1200×675 spp=500 d=50; CPU-ref speedup",
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -297,35 +465,17 @@ def main():
             "vs_baseline": None,
             "dtype": "f32" if fast else "f64",
             "data": "synthetic (the reference's own procedural final scene, fixed seed)",
-            "config": {"workload": f"complex_{W}x{H}_s{s}_d{DEPTH}", "width": W, "height": H,
+            "config": {"workload": workload_name(a), "width": W, "height": H,
                        "samples_sqrt": s, "spp": n_off, "max_depth": DEPTH,
                        "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED, "frames": frames,
-                       "parallelism": (f"frame-per-rank x{world} (render seed SEED+rank), no collective"
-                                       if weak else f"row-cyclic x{world}" +
-                                       (" + rccl all_gather" if world > 1 else "")),
+                       "parallelism": plan.describe(),
                        "mode": ("fast_f32 (statistical parity; xoroshiro64** per (pixel, sample))"
                                 if fast else "parity_f64 (bit-exact)")},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": peak,
-                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": traffic,
-                         "kernel": "rtw_fast_render" if fast else "rtw_render_persist (+ 7 small launches)",
-                         "kernel_ms": round(kms, 3),
-                         "algorithmic_flop_per_launch": brute_flop,
-                         "executed_flop_per_launch": exec_flop,
-                         "executed_tflops": round(executed, 3),
-                         "executed_frac_of_fp32_peak": round(executed / FP32_VECTOR_PEAK, 4),
-                         "note": ("fast mode: achieved = the same algorithmic brute-force work (segments x "
-                                  "n_spheres x 17 FLOP) in f32 / kernel time, against the FP32 vector peak"
-                                  if fast else None) or "achieved = SURVEY 8(d)'s algorithmic work (segments x n_spheres x 17 "
-                                 "FLOP, the reference's f64 brute-force Scene::hit) / HIP-event kernel "
-                                 "time, against the FP64 vector peak (parity mode is f64). The exact BVH "
-                                 "and f32 filter reach that rate without executing it "
-                                 "(executed_flop_per_launch: walk visits x 20 + exact f64 tests x 17), so "
-                                 "frac is an effective rate, not pipe utilisation. What bounds the launch "
-                                 "is VALU issue + latency of divergent per-lane work at 3 waves/SIMD "
-                                 "(valu_issue.simd_busy_frac, DESIGN.md 4)",
-                         "valu_issue": valu},
+            "roofline": roofline(a, st, kms, st.main_kernel_ms or kms, pm, pm_source, n_cu, st.grid_blocks),
+            "parity": parity,
+            "build_id": rtw.build_id(),
             "stats": {"accel": ["scan_f64", "scan_f32_filter", "bvh"][st.accel],
+                      "rank0_pixels": st.pixels,
                       "node_visits_per_segment": round(st.node_visits / max(1, st.segments), 3),
                       "brute_segments": st.brute_segments, "lds_bytes": st.lds_bytes,
                       "parked_pixels": st.parked_pixels,
@@ -333,20 +483,16 @@ def main():
                       "lane_utilization": round(st.segments / max(1, 64 * st.wave_iterations), 4),
                       "exact_tests_per_segment": round(st.exact_tests / max(1, st.segments), 3),
                       "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
-                      **({"walk_wave_iters_per_wave_iteration": round(st.exact_wave_iterations /
-                                                                      max(1, st.wave_iterations), 3)}
-                         if fast else {}),
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),
                       "trap_skipped_fraction": round(st.trap_segments / max(1, st.segments), 4)},
         }
-    if rank == 0 and world == 1 and a.e2e:
-        out["end_to_end"] = end_to_end(cam.raw, sph, ns, mt, nm, s, render_seed, fast, kms)
-    if rank == 0 and world == 1 and a.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)
-        out["cpu_baseline"]["gpu_speedup"] = round(value / out["cpu_baseline"]["value"], 1)
-        cl = out["cpu_baseline"]["clean_scheduler"]
-        cl["gpu_speedup"] = round(value / cl["value"], 1)
-    if rank == 0:
+        if world == 1 and a.e2e:
+            out["end_to_end"] = end_to_end(rtw, cam.raw, sph, ns, mt, nm, s, plan.render_seed, fast, kms, W * H)
+        if world == 1 and a.cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cam.raw, sph, ns, mt, nm, s, a.cpu_row_stride)
+            out["cpu_baseline"]["gpu_speedup"] = round(value / out["cpu_baseline"]["value"], 1)
+            cl = out["cpu_baseline"]["clean_scheduler"]
+            cl["gpu_speedup"] = round(value / cl["value"], 1)
         print(json.dumps(out), flush=True)
     sess.close()
     if world > 1:

@@ -12,15 +12,22 @@
 // reference's order, division and sqrt are IEEE (checked on the box by
 // rtw_probe_f64_ops). The RNG is the reference's u128 xorshift(23,17,26), bit-exact.
 //
-// Layout: one work-item per pixel, a 256-thread workgroup = a 16x16 pixel tile
-// (each wave64 = 16x4 pixels, neighbours with similar path lengths). The sphere
-// list {cx,cy,cz,r*r} (32 B each) is staged in LDS once per workgroup and read
-// with wave-uniform broadcasts; radius, material index and the material table stay
-// in HBM (read once per hit). Each lane runs a flattened sample x bounce loop:
-// one brute-force intersection pass per iteration, then scatter or finish the
-// sample and generate the next; the wave retires when all its lanes are done.
-// The ray_color product att0*(att1*(...*leaf)) is formed right-to-left from a
-// per-lane stack of material indices, so it associates exactly as the recursion.
+// Launches per render: rtw_seed_pixels (per-pixel RNG children by
+// GF(2) jump-ahead), the cost probe + 6 small kernels that order the pixels by
+// estimated cost, then rtw_render_persist -- the hot path. One 768-thread workgroup
+// per CU stages the scene in LDS once (BVH nodes + leaves, f64 sphere records,
+// shading records, pass-1 filter records) and keeps per-lane areas there (pixel
+// sum, walk scratch, speculative RNG state). Cursor waves run one pixel per lane
+// and refill idle lanes from a global cursor in cost order; a lane runs one
+// segment per wave iteration: Scene::hit by the exact-result 4-wide BVH
+// (rtw_accel.h), the scatter, and ONE rejection loop for every lane's draws.
+// Pixels whose serial sample chain runs long park at a sample boundary in a
+// write-through queue and are finished by whole waves (priority waves, then every
+// wave once the cursor is dry). The ray_color product att0*(att1*(...*leaf)) is
+// formed right-to-left from a per-path stack of sphere indices, so it associates
+// exactly as the recursion. rtw_park_leftover finishes any parked pixel nobody
+// claimed. The tile kernel (rtw_render_f64 + rtw_finish_parked, RTW_PERSIST=0)
+// stays for A/B and tests.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -149,9 +156,10 @@ struct KParams {
     const double4 *trap;        // per sphere rtw_accel::TrapRec {w, cap}
     const uint4 *jump;          // [jump_bits][128] columns of T^(2^k)
     double *out;                // n_rows * W * 3
-    uint16_t *spill;            // path-stack levels >= kRegSlots, region A: [level][pixel]
-    uint16_t *spill_b;          // region B (cooperative groups): [level][column]
-    uint64_t spill_stride;      // columns per level: max(pixels, persistent lanes)
+    uint16_t *spill;            // path-stack levels >= kRegSlots, region A (spill_idx)
+    uint16_t *spill_b;          // region B (cooperative groups)
+    uint64_t spill_stride;      // levels per column (lane-major; RTW_SPILL_LEVEL_MAJOR builds:
+                                // columns per level)
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
     uint64_t *stamps_coop;      // RTW_STAMPS builds only: phase-2 waves [wave][8]
     struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
@@ -289,20 +297,33 @@ constexpr uint32_t kRegSlots = 8;
 // another therefore never writes bytes that the first XCD's L2 may still hold
 // dirty (the L2s are not coherent with each other), and plain cached accesses
 // stay correct.
+// Spill slot of stack level l (>= kRegSlots) in column col. Lane-major: a column's
+// levels are contiguous (max_depth - kRegSlots u16 each), so a deep path dirties one
+// or two cache lines instead of one line per level -- the lanes of a persistent
+// wave push at different times, so the level-major layout's coalescing never
+// happened there, and its ~84 MB of level rows were written back line by line
+// (RTW_SPILL_LEVEL_MAJOR=1 builds keep it for A/B).
+__device__ __forceinline__ uint64_t spill_idx(uint32_t level, uint64_t col, uint64_t stride) {
+#ifdef RTW_SPILL_LEVEL_MAJOR
+    return static_cast<uint64_t>(level - kRegSlots) * stride + col;
+#else
+    return col * stride + (level - kRegSlots);
+#endif
+}
 struct PathStack {
     uint64_t r0 = 0, r1 = 0;
     uint32_t n = 0;
     __device__ __forceinline__ void push(uint32_t v, uint16_t *spill, uint64_t stride, uint64_t col) {
         if (n < 4) r0 |= static_cast<uint64_t>(v) << (16u * n);
         else if (n < kRegSlots) r1 |= static_cast<uint64_t>(v) << (16u * (n - 4u));
-        else spill[static_cast<uint64_t>(n - kRegSlots) * stride + col] = static_cast<uint16_t>(v);
+        else spill[spill_idx(n, col, stride)] = static_cast<uint16_t>(v);
         ++n;
     }
     __device__ __forceinline__ uint32_t at(uint32_t j, const uint16_t *spill, uint64_t stride,
                                            uint64_t col) const {
         if (j < 4) return static_cast<uint32_t>(r0 >> (16u * j)) & 0xffffu;
         if (j < kRegSlots) return static_cast<uint32_t>(r1 >> (16u * (j - 4u))) & 0xffffu;
-        return spill[static_cast<uint64_t>(j - kRegSlots) * stride + col];
+        return spill[spill_idx(j, col, stride)];
     }
     __device__ __forceinline__ void clear() { r0 = r1 = 0, n = 0; }
 };
@@ -677,7 +698,7 @@ __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, 
                                      uint64_t col, uint64_t stride, double &lr, double &lg, double &lb) {
     const uint32_t n = p.stk.n;
     for (uint32_t j = n; j-- > kRegSlots;) {
-        const ShadeRec &A = shd[spill[static_cast<uint64_t>(j - kRegSlots) * stride + col]];
+        const ShadeRec &A = shd[spill[spill_idx(j, col, stride)]];
         lr = A.a0 * lr;
         lg = A.a1 * lg;
         lb = A.a2 * lb;
@@ -1311,7 +1332,12 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
     const SceneView sv = stage_scene<kLds, kBvh>(P, lds_sph);
     uint16_t *scol = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lds_sph) + P.lane_lds_off) + threadIdx.x;
     // probe_sub > 1: one probed pixel per probe_sub x probe_sub block stands for the
-    // block in its tile's cost (the others keep pcost 0: ordered with their tile)
+    // block in its tile's cost (the others keep pcost 0: ordered with their tile).
+    // Hand-out order only, never the image. The estimate is biased when probe_sub
+    // does not divide the 8x8 order tile (a straddling block puts its whole weight on
+    // the probed pixel's tile) and a hot probed pixel counts 1, not its block's
+    // weight; the default (1) is exact, and RTW_PROBE_SUB > 1 stays an A/B knob
+    // (2: neutral, 3: +18 %, profiles/r02_misc/knob_probe_sub.log).
     const uint32_t sub = P.probe_sub > 1u ? P.probe_sub : 1u;
     const uint32_t wq = (P.W + sub - 1u) / sub, hq = (P.n_rows + sub - 1u) / sub;
     const uint64_t nq = static_cast<uint64_t>(wq) * hq;
@@ -2325,7 +2351,11 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
     P.spill = s->d_spill;
     P.spill_b = s->d_spill ? s->d_spill + spill_need / (2 * sizeof(uint16_t)) : nullptr;
+#ifdef RTW_SPILL_LEVEL_MAJOR
     P.spill_stride = spill_cols;
+#else
+    P.spill_stride = cam->max_depth > kRegSlots ? cam->max_depth - kRegSlots : 0;
+#endif
     // park queue (one slot per pixel) and the per-pixel segment budget of phase 1
     const size_t npix_sh = static_cast<size_t>(sh.n_rows) * cam->img_width;
     if (npix_sh > s->park_cap) {

@@ -1,9 +1,6 @@
-"""Multi-GPU work split: frames per rank, or one frame's rows.
+"""Multi-GPU work split: one frame's rows, or frames per rank.
 
-Weak scaling (bench.py default): an N-rank job renders N frames of the workload,
-one whole frame per rank (frame_seed); no data-path collective.
-
-Row-cyclic sharding of one frame (bench.py --scaling strong, BASELINE configs[3]):
+Row-cyclic sharding of one frame (bench.py default, BASELINE configs[3]):
 
 Pixels are independent and each pixel's RNG stream depends only on its global
 index (copy_reset chain, camera.rs:269-272), so any row partition reproduces the
@@ -11,6 +8,12 @@ single-GPU image bit-for-bit. Rows go to ranks cyclically (row r -> rank r % N)
 because sky rows are ~3x cheaper than ground rows. The one exchange is a gather
 of the row tiles (RCCL all_gather over xGMI on GPUs, gloo in CPU tests),
 followed by an un-permute on the receiving rank.
+
+Weak scaling (bench.py --scaling weak): an N-rank job renders N frames of the
+workload, one whole frame per rank (frame_seed); no data-path collective.
+
+StepPlan + step() are what bench.py runs per timed step; tests/test_shard_dist.py
+drives the same code over gloo with the oracle standing in for the GPU render.
 """
 from __future__ import annotations
 
@@ -66,3 +69,48 @@ def gather_image(tile, world: int, height: int, gathered=None, image=None, index
         image = torch.empty((height,) + tuple(tile.shape[1:]), dtype=tile.dtype, device=tile.device)
     image.index_copy_(0, dst, gathered.index_select(0, src))
     return image
+
+
+class StepPlan:
+    """One rank's share of a bench step: its shard, render seed, device tile and --
+    for N>1 strong scaling -- the gather buffers and the assembled image."""
+
+    def __init__(self, world: int, rank: int, height: int, width: int, weak: bool, seed: int,
+                 dtype, device):
+        import torch
+
+        self.world, self.rank, self.height, self.weak = world, rank, height, weak
+        if weak:  # frame `rank` of an N-frame job, the whole image on this rank
+            self.shard = (0, 1, height)
+            rows = height
+            self.render_seed = frame_seed(seed, rank)
+        else:  # row-cyclic shard of the one frame
+            self.shard = rows_of(rank, world, height)
+            rows = rows_max(world, height)  # tiles padded to the same row count
+            self.render_seed = seed
+        self.tile = torch.zeros((rows, width, 3), dtype=dtype, device=device)
+        self.collective = world > 1 and not weak
+        if self.collective:
+            self.gathered = torch.empty((world * rows, width, 3), dtype=dtype, device=device)
+            self.image = torch.empty((height, width, 3), dtype=dtype, device=device)
+            self.index = unpermute_index(world, height, device)
+        else:
+            self.image = self.tile
+
+    def gather(self):
+        if self.collective:
+            gather_image(self.tile, self.world, self.height, self.gathered, self.image, self.index)
+        return self.image
+
+    def describe(self) -> str:
+        if self.weak:
+            return f"frame-per-rank x{self.world} (render seed SEED+rank), no collective"
+        return f"row-cyclic x{self.world}" + (" + rccl all_gather" if self.world > 1 else "")
+
+
+def step(plan: StepPlan, render_tile, after_render=None):
+    """One bench step: render this rank's rows into plan.tile, then the gather."""
+    render_tile(plan)
+    if after_render is not None:
+        after_render()
+    return plan.gather()

@@ -40,9 +40,14 @@ def exe():
     return EXE
 
 
+# both candidate lists: the default device build's (0) and -DRTW_SELF_SKIP's (1)
+@pytest.mark.parametrize("self_skip", [0, 1])
 @pytest.mark.parametrize("scene,seed,paths", SCENES)
-def test_walk_matches_scan(exe, scene, seed, paths):
-    p = subprocess.run([exe, scene, str(seed), str(paths)], capture_output=True, text=True, timeout=300)
+def test_walk_matches_scan(exe, scene, seed, paths, self_skip):
+    if self_skip and not (scene.startswith("complex") or scene in ("random:300", "touch:100")):
+        pytest.skip("self-skip variant: a representative subset")
+    p = subprocess.run([exe, scene, str(seed), str(paths), str(self_skip)], capture_output=True, text=True,
+                       timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["bvh"], r
@@ -53,6 +58,7 @@ def test_walk_matches_scan(exe, scene, seed, paths):
         # the walk replaces the 486-sphere scan by ~20 node/leaf tests
         assert r["visits_per_walk"] < 40, r
         assert r["fallbacks"] + r["overflows"] < r["rays"] // 1000, r
+    assert (r["self_skips"] > 0) == bool(self_skip) or scene not in ("complex", "random:300"), r
     if scene == "complex" or scene.startswith("touch:"):
         assert r["inside_cuts"] > r["rays"] // 10, r  # the inside cut was exercised
 

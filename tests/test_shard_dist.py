@@ -1,9 +1,9 @@
 """Multi-rank paths on the CPU over gloo (world_size 2 and 3), with the oracle (the
 GPU kernel's checker) as the renderer:
-- strong (bench.py --scaling strong): each rank renders its row-cyclic shard, the
-  tiles are all-gathered and un-permuted by the same code bench.py uses, and the
-  result equals the unsharded image bit-for-bit;
-- weak (bench.py default): rank r renders frame r of the job at
+- strong (bench.py default): each rank renders its row-cyclic shard, the tiles are
+  all-gathered and un-permuted by bench.py's own step code (shard.StepPlan /
+  shard.step), and the result equals the unsharded image bit-for-bit;
+- weak (bench.py --scaling weak): rank r renders frame r of the job at
   shard.frame_seed(SEED, r), frame 0 being the single-GPU workload."""
 import os
 import socket
@@ -34,15 +34,21 @@ def _scene():
 
 
 def _worker(rank, world, port, out):
+    """One rank of bench.py's default N>1 step (shard.StepPlan + shard.step), with the
+    oracle rendering the rank's rows in place of the GPU."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle_ctypes as orc
     cam, sph, mat, n = _scene()
-    rb, step, nr = shard.rows_of(rank, world, H)
-    tile_np, _ = orc.render(cam, sph, n, mat, n, S, SEED, rows=(rb, step, nr), nthreads=2)
-    tile = torch.zeros((shard.rows_max(world, H), W, 3), dtype=torch.float64)
-    tile[:nr] = torch.from_numpy(tile_np)
-    img = shard.gather_image(tile, world, H)
+    plan = shard.StepPlan(world, rank, H, W, False, SEED, torch.float64, "cpu")
+    assert plan.describe() == f"row-cyclic x{world} + rccl all_gather"
+
+    def render_tile(pl):
+        rb, step, nr = pl.shard
+        tile_np, _ = orc.render(cam, sph, n, mat, n, S, pl.render_seed, rows=(rb, step, nr), nthreads=2)
+        pl.tile[:nr] = torch.from_numpy(tile_np)
+
+    img = shard.step(plan, render_tile)
     if rank == 0:
         np.save(out, img.numpy())
     dist.barrier()
@@ -76,8 +82,14 @@ def _frame_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle_ctypes as orc
     cam, sph, mat, n = _scene()
-    fb, _ = orc.render(cam, sph, n, mat, n, S, shard.frame_seed(SEED, rank), nthreads=2)
-    frame = torch.from_numpy(fb)
+    plan = shard.StepPlan(world, rank, H, W, True, SEED, torch.float64, "cpu")
+    assert plan.shard == (0, 1, H) and not plan.collective
+
+    def render_tile(pl):
+        fb, _ = orc.render(cam, sph, n, mat, n, S, pl.render_seed, nthreads=2)
+        pl.tile[:] = torch.from_numpy(fb)
+
+    frame = shard.step(plan, render_tile).clone()
     frames = [torch.zeros_like(frame) for _ in range(world)]
     dist.all_gather(frames, frame)  # the test's check only: the bench's weak path has no collective
     if rank == 0:

@@ -24,6 +24,10 @@
 
 using namespace rtw_accel;
 
+// 1: mirror a -DRTW_SELF_SKIP device build (candidate list without the sphere a
+// segment leaves); 0 (default): the default device build's candidate list
+static bool g_self_skip = false;
+
 struct F4 {
     float x, y, z, w;
 };
@@ -116,7 +120,8 @@ static Hit accel(const Scene &S, const double o[3], const double d[3], Counts &k
         return brute(S, o, d);
     }
     ++k.walked;
-    if (prev >= 0) {  // the device drops the sphere a segment leaves (rtw_accel.h self_skip)
+    if (prev >= 0 && g_self_skip) {  // opt-in device builds (-DRTW_SELF_SKIP) drop the sphere a
+                                     // segment leaves (rtw_accel.h self_skip); default builds keep it
         const uint32_t p = static_cast<uint32_t>(prev);
         wr.skip = self_skip(prev, o[0], o[1], o[2], d[0], d[1], d[2], a, S.c[3 * p], S.c[3 * p + 1], S.c[3 * p + 2],
                             S.rr[p]);
@@ -181,9 +186,10 @@ static void finish_scene(Scene &S) {
 
 int main(int argc, char **argv) {
     if (argc < 4) {
-        fprintf(stderr, "usage: accel_check SCENE SEED N_PATHS\n");
+        fprintf(stderr, "usage: accel_check SCENE SEED N_PATHS [SELF_SKIP 0|1]\n");
         return 2;
     }
+    g_self_skip = argc > 4 ? std::atoi(argv[4]) != 0 : false;  // default: the default device build
     const std::string name = argv[1];
     const uint64_t seed = std::strtoull(argv[2], nullptr, 10);
     const uint64_t npaths = std::strtoull(argv[3], nullptr, 10);

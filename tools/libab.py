@@ -20,7 +20,7 @@ def main():
         for lib in libs:
             env = dict(os.environ, RTW_LIB=os.path.abspath(lib))
             p = subprocess.run([sys.executable, os.path.join(HERE, "bench.py"), "--steps", "3", "--warmup", "1",
-                                "--cpu-baseline", "0"] + os.environ.get("LIBAB_ARGS", "").split(), env=env, capture_output=True, text=True, timeout=300)
+                                "--cpu-baseline", "0", "--pmc", "0", "--e2e", "0"] + os.environ.get("LIBAB_ARGS", "").split(), env=env, capture_output=True, text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("{")]
             if p.returncode != 0 or not line:
                 print(f"{lib}: failed rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
