@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                    help="N>1: strong = the one frame row-cyclically sharded + RCCL all_gather "
                         "(BASELINE configs[3]); weak = one whole frame per rank (seed SEED+rank)")
+    p.add_argument("--shard-of", default="",
+                   help="N:r -- one process renders only rank r's rows of an N-rank strong split "
+                        "(a rank of a multi-GPU config measured on one GPU; the other ranks are not run)")
     p.add_argument("--mode", choices=("parity", "fast"), default="parity",
                    help="parity = f64 bit-exact (the headline); fast = the f32 mode with "
                         "independent per-sample streams (statistical parity, tests/test_gpu_fast.py)")
@@ -98,6 +101,7 @@ def parse():
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     a = p.parse_args()
     a.width, a.height = (int(v) for v in a.size.lower().split("x"))
+    a.sim = tuple(int(v) for v in a.shard_of.split(":")) if a.shard_of else None
     return a
 
 
@@ -389,7 +393,12 @@ def main():
     fdt = torch.float32 if fast else torch.float64
     sess = rtw.Session(local)
     sess.set_scene(sph, ns, mt, nm)
-    plan = shard.StepPlan(world, rank, H, W, weak, SEED, fdt, dev)
+    if a.sim:  # rank r of an N-rank split, alone on this GPU
+        if world > 1:
+            raise SystemExit("--shard-of is a single-process measurement")
+        plan = shard.StepPlan(a.sim[0], a.sim[1], H, W, False, SEED, fdt, dev, collective=False)
+    else:
+        plan = shard.StepPlan(world, rank, H, W, weak, SEED, fdt, dev)
     render = sess.render_fast if fast else sess.render
     stream = torch.cuda.current_stream(dev)
     kernel_ms = []
@@ -432,14 +441,18 @@ def main():
 
     frames = world if weak else 1
     total_samples = frames * W * H * n_off * a.steps
+    if a.sim:  # this rank's samples only
+        total_samples = st.pixels * n_off * a.steps
     value = total_samples / elapsed / 1e6
-    parity = parity_check(a, plan.image, segments) if rank == 0 else None
+    parity = parity_check(a, plan.image, segments) if rank == 0 and not a.sim else None
 
     out = None
     if rank == 0:
         pm, pm_source = None, "not collected (N>1)"
         n_cu = torch.cuda.get_device_properties(local).multi_processor_count
-        if world == 1:
+        if a.sim:
+            pm_source = "not collected (--shard-of: the counter child renders whole frames)"
+        elif world == 1:
             if a.pmc:
                 res, why = pmc_live(a)
                 if res and "insts" in res:
@@ -468,7 +481,9 @@ def main():
             "config": {"workload": workload_name(a), "width": W, "height": H,
                        "samples_sqrt": s, "spp": n_off, "max_depth": DEPTH,
                        "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED, "frames": frames,
-                       "parallelism": plan.describe(),
+                       "parallelism": (f"rank {a.sim[1]} of a row-cyclic x{a.sim[0]} split, alone on one "
+                                       "GPU (value = this rank's samples / its time; the other ranks "
+                                       "not run)" if a.sim else plan.describe()),
                        "mode": ("fast_f32 (statistical parity; xoroshiro64** per (pixel, sample))"
                                 if fast else "parity_f64 (bit-exact)")},
             "roofline": roofline(a, st, kms, st.main_kernel_ms or kms, pm, pm_source, n_cu, st.grid_blocks),

@@ -88,4 +88,20 @@ RTW_NHD void div3(double &x, double &y, double &z, double d) {
     x = x / d, y = y / d, z = z / d;
 }
 
+// Dielectric::scatter's "cannot refract" test, materials.rs:94-98:
+//   ratio * sqrt(1 - cos^2) > thr   (thr = 1; the trapped-path hint uses 1 + 1e-9)
+// decided without the square root when the squared comparison is clear by a
+// relative margin of 2^-30 -- the operations here err by a few 2^-53 each -- and
+// exactly as the reference (the square root, the product) otherwise, or when ratio
+// is not a moderate positive number. x = 1 - cos*cos is the reference's own operand.
+// Same decision for every input (tools/next01_check.cpp "tir" checks it).
+RTW_NHD bool tir_exceeds(double ratio, double x, double thr) {
+    if (ratio > 1e-100 && ratio < 1e100) {
+        const double q = (ratio * ratio) * x, t2 = thr * thr;
+        if (q > t2 * (1. + 0x1p-30)) return true;
+        if (q < t2 * (1. - 0x1p-30)) return false;
+    }
+    return ratio * __builtin_sqrt(x) > thr;
+}
+
 }  // namespace rtw_num

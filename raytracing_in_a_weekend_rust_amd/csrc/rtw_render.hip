@@ -145,6 +145,9 @@ struct KParams {
     uint32_t probe_sub;         // cost probe on every probe_sub-th pixel of every probe_sub-th row
     uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
                                 // pixel; the leftover launch finishes them all
+    uint32_t drain_prio;        // draining waves raise their issue priority (RTW_DRAIN_PRIO, default 1)
+    uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
+                                // segments is parked before its first sample (0: off)
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
@@ -602,10 +605,11 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
         // with the reference's own IEEE operations: the same bits
         ratio = front ? M.a0 : M.p;
         cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
-        const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
-        refl = ratio * sin_t > 1.;
+        // ratio * sqrt(1 - cos^2) > 1, its square root taken only near the boundary
+        const double sin2 = 1.0 - cos_t * cos_t;
+        refl = rtw_num::tir_exceeds(ratio, sin2, 1.);
         if constexpr (kTrap) {  // TIR with margin, chords 2 r cos well above 0.01
-            th->tir = !front && ratio * sin_t > 1. + 1e-9 && r * cos_t > 0.0055;
+            th->tir = !front && refl && rtw_num::tir_exceeds(ratio, sin2, 1. + 1e-9) && r * cos_t > 0.0055;
         }
         if (!refl) {
             const double r0 = M.a1;
@@ -741,6 +745,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
     const PixelLoc pl(P, x, y);
     const uint64_t stride = P.spill_stride;
     Path p;
+    int tir_no = -1;  // kTrap: S whose great-circle test failed on the last TIR bounce
     gen_ray(P, pl, ps.k, ps.rng, p, stp);
     STAMP(0);  // 0: seed jump + pixel setup
     for (;;) {
@@ -754,8 +759,21 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         TrapHint th;
         bool done = shade<kTrap>(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp, &th);
         if constexpr (kTrap) {
-            if (!done && (th.lam || th.tir)) {
+            // a total internal reflection keeps the path in the great circle it walks
+            // (the chord, the normal and the reflection share S's centre), and the
+            // circle test of trap_forward does not depend on the position on it: after
+            // one failed test every further TIR bounce inside the same S fails too, so
+            // it is skipped (tir_no) until the path leaves the circle -- tracing on is
+            // always exact, the forward only saves work
+#ifdef RTW_NO_TIR_CACHE  // A/B: test every TIR bounce
+            const bool skip = false;
+#else
+            const bool skip = th.tir && best == tir_no;
+#endif
+            tir_no = -1;
+            if (!done && (th.lam || th.tir) && !skip) {
                 const uint32_t k = trap_forward(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
+                if (!k && th.tir) tir_no = best;
                 if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
             }
         }
@@ -835,33 +853,6 @@ struct Tally {
     uint32_t seg = 0, ntest = 0, nwave2 = 0, visits = 0, nbrute = 0, parked = 0, witer = 0, inside = 0,
              trap = 0;
 };
-
-// Inside cut (rtw_accel.h): the segment starts inside `prev`, the sphere it last
-// hit, and leaves it through the far root -- then only prev's list can come
-// nearer. Returns true with the scan's (best, bt) if the cut applies.
-__device__ __forceinline__ bool inside_hit(const double4 *__restrict__ sph, const ShadeRec *__restrict__ shd,
-                                           const uint16_t *__restrict__ nbr, int prev, double ox, double oy,
-                                           double oz, double dx, double dy, double dz, double a, int &best,
-                                           double &bt, Tally &tl, bool count = true) {
-    if (prev < 0) return false;
-    const uint32_t info = shd[prev].nbr;
-    if (info == rtw_accel::kNbrNone) return false;
-    const double4 S = sph[prev];
-    double t;
-    if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t)) return false;
-    const uint32_t n = info & 0xffu;
-    if (count) tl.inside += 1u, tl.ntest += 1u + n;
-    best = prev, bt = t;
-    const uint16_t *l = nbr + (info >> 8);
-    for (uint32_t j = 0; j < n; ++j) {
-        const uint32_t i = l[j];
-        const double4 T = sph[i];
-        if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w, t) &&
-            rtw_accel::better(t, i, bt, best))
-            bt = t, best = static_cast<int>(i);
-    }
-    return true;
-}
 
 // The scan: every sphere in index order (first = lane's sub-range start, step =
 // sphere stride for cooperative groups); pass 1 = f32 filter on wave-uniform
@@ -1187,6 +1178,41 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
     if (kG >= 64) shfl_min_step(bt, best, 32);
 }
 
+// Inside cut (rtw_accel.h): the segment starts inside `prev`, the sphere it last
+// hit, and leaves it through the far root -- then only prev's list can come
+// nearer: the scan's (best, bt) is the (t, index) minimum over prev and its list.
+// Used by cooperative groups: every lane of the group holds the same path, so S's
+// far root is formed on every lane, and lane j of the group
+// tests entry j of S's list (at most rtw_accel::kMaxNbr <= kG entries) -- the list's
+// exact tests run side by side instead of one after another on the pixel's serial
+// chain -- then the group's (t, index) minimum. Same result as inside_hit.
+template <uint32_t kG>
+__device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph, const ShadeRec *__restrict__ shd,
+                                                 const uint16_t *__restrict__ nbr, int prev, double ox,
+                                                 double oy, double oz, double dx, double dy, double dz, double a,
+                                                 int &best, double &bt, Tally &tl, uint32_t sub) {
+    static_assert(rtw_accel::kMaxNbr <= kG, "one list entry per lane");
+    if (prev < 0) return false;
+    const uint32_t info = shd[prev].nbr;
+    if (info == rtw_accel::kNbrNone) return false;
+    const double4 S = sph[prev];
+    double t;
+    if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t)) return false;
+    const uint32_t n = info & 0xffu;  // group-uniform
+    if (sub == 0) tl.inside += 1u, tl.ntest += 1u + n;
+    best = prev, bt = t;
+    if (n == 0) return true;
+    if (sub < n) {
+        const uint32_t i = nbr[(info >> 8) + sub];
+        const double4 T = sph[i];
+        if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w, t) &&
+            rtw_accel::better(t, i, bt, best))
+            bt = t, best = static_cast<int>(i);
+    }
+    group_min<kG>(bt, best);
+    return true;
+}
+
 // Phase 2: the parked pixels, kG lanes per pixel. Persistent groups take pixels
 // in park order (the heaviest parked first) from an atomic cursor. Scene::hit is
 // split across the group: lane j filters spheres j, j + kG, ... against the
@@ -1224,7 +1250,8 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         bt = 0.;
         // inside cut: every lane of the group holds the same path, so the branch
         // is group-uniform and the lanes run the (short) list redundantly
-        if (inside_hit(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl, sub == 0)) return best;
+        if (inside_hit_group<kG>(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl, sub))
+            return best;
         const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
         STAMP(0);  // coop: loop back + segment setup (Seg32)
         if (rec_in_regs) {
@@ -1579,6 +1606,15 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     if (P.max_depth == 0) {  // every sample black, no Scene::hit call
                         ps.k = P.n_off;
                         write_pixel(P, x, lr, ps);
+                    } else if (P.prepark && order_map && KP(pcost)[pix] >= P.prepark) {
+                        // a long serial chain by the probe's estimate: to a drain wave
+                        // from its first sample
+                        Parked q;
+                        q.x = x, q.lr = lr, q.k = 0, q._pad = 0;
+                        q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
+                        q.ar = q.ag = q.ab = 0., q._pad2 = 0.;
+                        publish_parked(P, q);
+                        ++tl.parked;
                     } else {
                         gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), 0, ps.rng, p, stp);
                         need = false;
@@ -1647,8 +1683,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 } else if (kind == RTW_DIELECTRIC) {  // materials.rs:83-111 (attenuation 1)
                     const double ratio = front ? M.a0 : M.p;  // host: a0 = 1/ir, a1 = r0*r0
                     const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
-                    const double sin_t = __builtin_sqrt(1.0 - cos_t * cos_t);
-                    bool refl = ratio * sin_t > 1.;
+                    // ratio * sqrt(1 - cos^2) > 1, the square root only near the boundary
+                    bool refl = rtw_num::tir_exceeds(ratio, 1.0 - cos_t * cos_t, 1.);
                     if (!refl) {
                         const double r0 = M.a1;
                         const double q = 1. - cos_t;
@@ -1845,6 +1881,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     uint32_t cseg = 0;
     // RTW_DRAIN_OFF=1 (tests): no drain here, so every parked pixel is left to the
     // follow-up launch (rtw_park_leftover) -- that path then runs on every entry
+    // a wave that drains runs one pixel's serial chain for the whole wave: raised
+    // issue priority (as the priority waves), so the chains that set the launch's end
+    // are not held back by the cursor waves still sharing the SIMD (RTW_DRAIN_PRIO=0: off)
+    if (KP(drain_prio)) __builtin_amdgcn_s_setprio(3);
     for (bool drain = !KP(drain_off); drain;) {
         uint32_t t = 0, state = 0;  // state 1: ticket t is published, 2: stop
         if (sub == 0) {
@@ -2562,6 +2602,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
+        P.drain_prio = 1;
+        if (const char *e = std::getenv("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = std::atoi(e) != 0 ? 1u : 0u;
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};

@@ -76,7 +76,7 @@ class StepPlan:
     for N>1 strong scaling -- the gather buffers and the assembled image."""
 
     def __init__(self, world: int, rank: int, height: int, width: int, weak: bool, seed: int,
-                 dtype, device):
+                 dtype, device, collective: bool = True):
         import torch
 
         self.world, self.rank, self.height, self.weak = world, rank, height, weak
@@ -89,7 +89,7 @@ class StepPlan:
             rows = rows_max(world, height)  # tiles padded to the same row count
             self.render_seed = seed
         self.tile = torch.zeros((rows, width, 3), dtype=dtype, device=device)
-        self.collective = world > 1 and not weak
+        self.collective = collective and world > 1 and not weak
         if self.collective:
             self.gathered = torch.empty((world * rows, width, 3), dtype=dtype, device=device)
             self.image = torch.empty((height, width, 3), dtype=dtype, device=device)

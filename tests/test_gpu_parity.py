@@ -200,6 +200,7 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0", "endgame"), ("2", "0.3", "endgame"),  # dry cursor: park everything (RTW_ENDGAME)
     ("2", "0", "endgame_coopg16"),
     ("2", "0", "probe2"), ("2", "0.3", "probe3"),  # cost probe on one pixel per 2x2 / 3x3 block
+    ("2", "0", "prepark"), ("2", "0", "drainprio0"),  # probe-hot pixels parked at once; drain at prio 0
 ]
 
 
@@ -220,6 +221,8 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     endgame = coop.startswith("endgame")
     monkeypatch.setenv("RTW_ENDGAME", "100000000" if endgame else "0")
     monkeypatch.setenv("RTW_PROBE_SUB", coop[5:] if coop.startswith("probe") else "1")
+    monkeypatch.setenv("RTW_PREPARK", "4" if coop == "prepark" else "0")
+    monkeypatch.setenv("RTW_DRAIN_PRIO", "0" if coop == "drainprio0" else "1")
     if coop == "endgame_coopg16":
         monkeypatch.setenv("RTW_COOPG", "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
@@ -229,8 +232,10 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     assert st.accel == int(accel)
     if budget == "0.01":
         assert st.parked_pixels == 45 * 80
-    if budget == "0" and coop != "rate1" and not endgame:
+    if budget == "0" and coop not in ("rate1", "prepark") and not endgame:
         assert st.parked_pixels == 0
+    if coop == "prepark":
+        assert st.parked_pixels > 45 * 80 // 4
     if endgame:
         assert st.parked_pixels > 0
     if coop == "rate1":
