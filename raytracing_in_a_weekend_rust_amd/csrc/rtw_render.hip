@@ -61,7 +61,7 @@ constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
-constexpr int kCounters = 12;
+constexpr int kCounters = 16;  // [11..15]: RTW_WALK_DIAG builds only
 // park a pixel past this many segments x samples per pixel (10 -> 14 in round 2: the
 // faster kernel leaves fewer pixels worth a whole drain wave; 12-17 all 151.4-151.5 ms
 // vs 153.2 ms at 10, interleaved A/B, profiles/r02_misc/knobs_budget.log)
@@ -146,6 +146,8 @@ struct KParams {
     uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
                                 // pixel; the leftover launch finishes them all
     uint32_t drain_prio;        // draining waves raise their issue priority (RTW_DRAIN_PRIO, default 1)
+    uint32_t hot_tickets;       // waves holding one of the first hot_tickets pixels of the cost order
+                                // run at raised priority (0: off)
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
                                 // segments is parked before its first sample (0: off)
     uint64_t seed_lo, seed_hi;
@@ -1226,6 +1228,9 @@ template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, const Parked &q,
                                                uint64_t col, Tally &tl, Stamps &stp) {
+#ifdef RTW_DIAG_NO_COOP  // register-pressure experiment only: the cursor path alone
+    return 0;
+#endif
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
@@ -1567,6 +1572,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
         uint32_t x = 0, lr = 0, pseg = 0;
         bool spec = false;  // spec_lds holds the state the lane's next unit vector draws from
+        bool hotpix = false;   // the lane's pixel is among the first hot_tickets of the cost order
+        bool wave_hot = false; // wave-uniform: the wave runs at raised priority for them
         uint64_t pix = 0;
         PixelState ps;
         Path p;
@@ -1583,6 +1590,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 if (rank == 0) base = atomicAdd(KP(pix_cursor), static_cast<uint32_t>(__popcll(m)));
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
+                hotpix = ticket < P.hot_tickets;
                 if (ticket < npix) {
                     // hand-out order: by descending estimated cost (P.order_map,
                     // rtw_cost_probe), so the cheapest pixels fill the drain; else
@@ -1624,6 +1632,17 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
             }
             dry = dry || __any(dry_now);  // wave-uniform
+            if (P.hot_tickets) {
+                // a wave holding one of the costliest pixels (the first hot_tickets of the
+                // cost order: the longest serial chains) issues at raised priority, so the
+                // chains that end the launch get more of their SIMD (RTW_HOT_PRIO)
+                const bool h = __any(!need && hotpix);
+                if (h != wave_hot) {
+                    wave_hot = h;
+                    if (h) __builtin_amdgcn_s_setprio(2);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+            }
             // endgame: once the cursor is dry and at most P.endgame pixels of the shard
             // are unfinished (about one per drain group), every lane parks its pixel
             // at its next sample boundary -- the last chains then run on a whole wave
@@ -1640,7 +1659,30 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
             double bt = 0.;
             STAMP(0);  // 0: loop top, refill
+#ifdef RTW_WALK_DIAG  // diagnostic build: the wave's walk length with and without its camera rays
+            const uint32_t v_before = tl.visits;
+#endif
             const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
+#ifdef RTW_WALK_DIAG
+            {
+                const uint32_t v = tl.visits - v_before;
+                const bool prim = p.depth == 0;
+                uint32_t m_all = v, m_sec = prim ? 0u : v, m_prim = prim ? v : 0u;
+                for (int off = 32; off > 0; off >>= 1) {
+                    m_all = max(m_all, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m_all), off)));
+                    m_sec = max(m_sec, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m_sec), off)));
+                    m_prim = max(m_prim, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m_prim), off)));
+                }
+                const uint64_t pm = __ballot(prim);
+                if (lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1)) {
+                    atomicAdd(&P.counters[11], static_cast<unsigned long long>(m_all));
+                    atomicAdd(&P.counters[12], static_cast<unsigned long long>(m_sec));
+                    atomicAdd(&P.counters[13], static_cast<unsigned long long>(m_prim));
+                    atomicAdd(&P.counters[14], static_cast<unsigned long long>(__popcll(pm)));
+                }
+                if (prim) atomicAdd(&P.counters[15], static_cast<unsigned long long>(v));
+            }
+#endif
             STAMP(1);  // 1: hit tail (exact candidates, cut check)
             // ---- segment end: HitRecord + scatter (materials.rs:22-111) or the sky, the
             // sample boundary, and ONE rejection loop for every lane's draws --
@@ -2563,12 +2605,19 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // iterations), and the waves left without a pixel drain the park queue
         // heavy waves per workgroup (RTW_HEAVY, default 2): raised priority, parked
         // pixels only. A shard with fewer pixels than cursor lanes (strong scaling
-        // at N >= 8) leaves whole waves without a pixel from the start: those drain
-        // the park queue, so no wave is reserved and no pixel is parked for being
-        // late (dry-cursor parking off) -- measured 86 vs 93 ms per rank at N=8.
+        // at N >= 8) leaves whole waves without a pixel from the start; they drain
+        // the park queue too, and no pixel is parked for being late (dry-cursor
+        // parking off). Since draining waves raise their priority (drain_prio) the
+        // priority waves pay there as well: N=8 rank 54.7 (0) -> 52.2 ms (2), and at
+        // N=1 they are worth 15 % (1: 152 ms, 2: 128 ms; profiles/r03_drain1).
         const uint32_t wpb = static_cast<uint32_t>(pblock) / 64u;
         const bool small_shard = npix < static_cast<uint64_t>(grid_p) * (wpb - kHeavyPerBlock) * 64u;
-        uint32_t heavy = small_shard ? 0u : kHeavyPerBlock;
+        // A shard of about one pixel per lane (N=4 of the bench image) takes a third
+        // priority wave: its medium chains all start at once and the drain has more to
+        // take (rank 70.2 -> 66-69 ms; N=1, 2, 8 lose with it: profiles/r03_misc/
+        // knobs_heavy_rate_endgame.log, knobs_hot_prio_endgame.log)
+        const double fill = static_cast<double>(npix) / (static_cast<double>(grid_p) * pblock);
+        uint32_t heavy = fill >= 0.75 && fill < 1.5 ? kHeavyPerBlock + 1u : kHeavyPerBlock;
         if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
@@ -2604,6 +2653,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (const char *e = std::getenv("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
         P.drain_prio = 1;
         if (const char *e = std::getenv("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = std::getenv("RTW_HOT_PRIO"))  // percent of the shard's pixels
+            P.hot_tickets = P.order_map ? static_cast<uint32_t>(std::atof(e) / 100. * static_cast<double>(npix)) : 0u;
         if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = std::atoi(e) != 0 ? 1u : 0u;
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
@@ -2783,6 +2834,11 @@ void collect(rtw_session *s) {
     }
     unsigned long long c[kCounters] = {};
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
+#ifdef RTW_WALK_DIAG
+    std::fprintf(stderr, "walk_diag: wave-iters %llu, sum max visits all %llu, without camera rays %llu, "
+                         "camera rays only %llu; camera-ray segments %llu, their visits %llu\n",
+                 c[1], c[11], c[12], c[13], c[14], c[15]);
+#endif
     float ms = 0.f;
     HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
     s->last.segments = c[0];

@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-knob_ab}; mkdir -p $OUT
 R=$1; shift
 for i in $(seq 1 $R); do
   for e in "$@"; do
-    ms=$(env $e timeout -k 10 200 python bench.py --cpu-baseline 0 --e2e 0 --steps 3 --warmup 1 | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['roofline']['kernel_ms'])")
+    ms=$(env $e timeout -k 10 200 python bench.py --cpu-baseline 0 --e2e 0 --pmc 0 --steps 3 --warmup 1 | python -c "import json,sys;d=json.loads(sys.stdin.read());print(d['roofline']['kernel_ms'])")
     echo "[$e] $ms" | tee -a $OUT/log.txt
   done
 done
