@@ -61,7 +61,7 @@ constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
-constexpr int kCounters = 16;  // [11..15]: RTW_WALK_DIAG builds only
+constexpr int kCounters = 20;  // [11..19]: RTW_WALK_DIAG builds only
 // park a pixel past this many segments x samples per pixel (10 -> 14 in round 2: the
 // faster kernel leaves fewer pixels worth a whole drain wave; 12-17 all 151.4-151.5 ms
 // vs 153.2 ms at 10, interleaved A/B, profiles/r02_misc/knobs_budget.log)
@@ -146,6 +146,8 @@ struct KParams {
     uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
                                 // pixel; the leftover launch finishes them all
     uint32_t drain_prio;        // draining waves raise their issue priority (RTW_DRAIN_PRIO, default 1)
+    uint32_t plist_thlog, plist_tx;  // camera-ray lists: log2 of the tile height (shard rows),
+                                     // tiles per row (tiles are 8 pixels wide)
     uint32_t hot_tickets;       // waves holding one of the first hot_tickets pixels of the cost order
                                 // run at raised priority (0: off)
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
@@ -176,6 +178,8 @@ struct KParams {
     uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base;
                                 // then per tile: its hot pixels
     uint32_t *pcost;            // per pixel: probe segments
+    uint4 *plist;               // per tile: candidate spheres of its camera rays (rtw_primary_lists)
+                                // or null
     uint32_t *cost_hist;        // [kCostBuckets] counts, then bucket write cursors
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
@@ -897,11 +901,18 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 
 // Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
 // exact candidates, the cut check; anything unproven falls back to the scan.
+// Camera-ray candidate list of a tile (rtw_primary_lists): count in the low 16
+// bits of x (kListNone: no list, walk), then up to kListMax sphere indices, 16 bits
+// each, from the high half of x on.
+constexpr uint32_t kListMax = 7;
+constexpr uint32_t kListNone = 0xffffu;
+__device__ __forceinline__ uint4 no_list() { return make_uint4(kListNone, 0u, 0u, 0u); }
+
 template <bool kLdsStack = false>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
-                                       double *sa_out = nullptr) {
+                                       double *sa_out = nullptr, uint4 pl = no_list()) {
     const double4 *__restrict__ sph = sv.sph;
     const float4 *__restrict__ nodes = sv.nodes;
     const float4 *__restrict__ leaves = sv.leaves;
@@ -920,8 +931,13 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
         }
         STAMP(5);  // 5: segment setup + always-spheres
         rtw_accel::WalkRay wr;
+        // a camera ray (prev < 0) of a tile with a list: its candidates are the list --
+        // every BVH sphere any camera ray of the tile can hit -- and there is no walk
+        const uint32_t lcount = pl.x & 0xffffu;
+        const bool listed = prev < 0 && lcount != kListNone;
         if (KP(n_node) == 0) {  // every sphere is an "always" sphere
-        } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
+        } else if (!listed &&
+                   !rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
             brute = true;
         } else {
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
@@ -932,7 +948,18 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
             }
 #endif
             auto run = [&](auto &ws) {
-                const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
+                bool walked = true;
+                if (listed) {  // the list's spheres become the candidates (index order irrelevant:
+                               // the exact loop keeps the (t, index) minimum)
+                    const uint32_t w[4] = {pl.x >> 16, pl.y, pl.z, pl.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < kListMax; ++j) {
+                        const uint32_t id = (w[(j + 1u) >> 1] >> ((j & 1u) ? 0u : 16u)) & 0xffffu;
+                        ws.add_cand(j == 0 ? w[0] : id, j < lcount);
+                    }
+                } else {
+                    walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
+                }
                 STAMP(2);  // 2: BVH walk
                 if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
@@ -953,7 +980,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
             if (!walked) {
                 brute = true;
             } else {
-                brute = !rtw_accel::cut_ok(U, best, bt, g.sa);
+                brute = !listed && !rtw_accel::cut_ok(U, best, bt, g.sa);  // a list cut nothing
             }
         }
     }
@@ -1205,7 +1232,11 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
     best = prev, bt = t;
     if (n == 0) return true;
     if (sub < n) {
-        const uint32_t i = nbr[(info >> 8) + sub];
+        // the entry's address formed here: hoisted out of the pixel's loop, the
+        // compiler kept it through the whole chain and spilled it to scratch
+        uint32_t e = (info >> 8) + sub;
+        asm volatile("" : "+v"(e));
+        const uint32_t i = nbr[e];
         const double4 T = sph[i];
         if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w, t) &&
             rtw_accel::better(t, i, bt, best))
@@ -1459,6 +1490,96 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
     if (mine) P.order_map[P.cost[t] + static_cast<uint32_t>(__popcll(m & ((1ull << r) - 1ull)))] = static_cast<uint32_t>(i);
 }
 
+// Camera-ray candidate lists. Every sample's first segment (get_ray, camera.rs:
+// 400-420) starts on the defocus disk o = look_from + ddu px + ddv py (|p| < 1) and
+// passes through a sample point s in its pixel's square (pixel00 + du (i + a) +
+// dv (j + b), a, b in [0, 1]: the lattice offsets lie inside it, camera.rs:422-450);
+// its points are (1 - t) o + t s for t >= 0.01 (interval.rs:55-57). In the camera
+// frame (u, v, depth along -w) a tile of pixels then bounds, for every t, the
+// lateral coordinates by t s_lo - |1 - t| R and t s_hi + |1 - t| R (R: the disk's
+// extent along the axis): a concave and a convex piecewise-linear bound, so over a
+// t interval their extremes sit at its ends. A BVH sphere is listed iff its padded
+// camera-frame box meets that region for some t whose depth reaches its depth slab.
+// The padding (2^-20 of the sphere's distance + radius, beyond the f64 Sphere::hit's
+// tangent-ray error ~2^-26.5 |oc|, plus an absolute slack) keeps the list a superset
+// of the spheres any camera ray of the tile can hit in the reference's f64
+// arithmetic. More than kListMax spheres, or a degenerate camera: no list (walk).
+struct PrimFrame {
+    double from[3], u[3], v[3], w[3];  // look_from and the camera basis (camera.rs:96-100)
+    double ru, rv, rz;                 // |o - look_from| along u, v, w (padded)
+    double eps;                        // absolute slack of every bound
+    uint32_t tw, th, tx, ty;           // tile width (pixels) and height (shard rows); tiles
+};
+__global__ __launch_bounds__(kBlock) void rtw_primary_lists(const KParams P, const PrimFrame F) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= F.tx * F.ty) return;
+    const uint32_t tyi = t / F.tx, txi = t - tyi * F.tx;
+    const uint32_t x0 = txi * F.tw, x1 = min(x0 + F.tw, P.W) - 1u;
+    const uint32_t lr0 = tyi * F.th, lr1 = min(lr0 + F.th, P.n_rows) - 1u;
+    const uint32_t y0 = P.row_begin + lr0 * P.row_step, y1 = P.row_begin + lr1 * P.row_step;
+    const CamRef C(P);
+    // the tile's sample points relative to look_from, bounded along one axis e
+    double q[3];
+    for (int k = 0; k < 3; ++k)
+        q[k] = ((C(C.kP00 + k) + C(C.kDu + k) * static_cast<double>(x0)) + C(C.kDv + k) * static_cast<double>(y0)) -
+               F.from[k];
+    const double nx = static_cast<double>(x1 + 1u - x0), ny = static_cast<double>(y1 + 1u - y0);
+    auto range = [&](const double *e, double sgn, double &lo, double &hi) {
+        const double base = sgn * (q[0] * e[0] + q[1] * e[1] + q[2] * e[2]);
+        const double a = sgn * nx * (C(C.kDu) * e[0] + C(C.kDu + 1) * e[1] + C(C.kDu + 2) * e[2]);
+        const double b = sgn * ny * (C(C.kDv) * e[0] + C(C.kDv + 1) * e[1] + C(C.kDv + 2) * e[2]);
+        lo = base + fmin(a, 0.) + fmin(b, 0.) - F.eps;
+        hi = base + fmax(a, 0.) + fmax(b, 0.) + F.eps;
+    };
+    double ulo, uhi, vlo, vhi, zlo, zhi;
+    range(F.u, 1., ulo, uhi);
+    range(F.v, 1., vlo, vhi);
+    range(F.w, -1., zlo, zhi);  // depth along -w
+    uint4 out = make_uint4(kListNone, 0u, 0u, 0u);
+    if (zlo - F.rz > 0. && zhi < 1e300) {
+        const double inv_hi = 1. / (zhi + F.rz), inv_lo = 1. / (zlo - F.rz);
+        const double sU = fabs(ulo) + fabs(uhi) + F.ru, sV = fabs(vlo) + fabs(vhi) + F.rv;
+        uint32_t n = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+        const uint32_t nsph = P.n_sph, nal = P.n_always;
+        uint32_t ai = 0;
+        for (uint32_t k = 0; k < nsph; ++k) {  // wave-uniform
+            if (ai < nal && ld_const_u32(P.always, ai) == k) {  // tested before any walk anyway
+                ++ai;
+                continue;
+            }
+            const double4 S = P.sph[k];
+            const double r = fabs(P.shade[k].r);
+            const double dx = S.x - F.from[0], dy = S.y - F.from[1], dz = S.z - F.from[2];
+            const double cu = dx * F.u[0] + dy * F.u[1] + dz * F.u[2];
+            const double cv = dx * F.v[0] + dy * F.v[1] + dz * F.v[2];
+            const double cz = -(dx * F.w[0] + dy * F.w[1] + dz * F.w[2]);
+            const double rp = r + 0x1p-20 * (fabs(dx) + fabs(dy) + fabs(dz) + r) + F.eps;
+            double t0 = (cz - rp - F.rz) * inv_hi, t1 = (cz + rp + F.rz) * inv_lo;
+            t0 = fmax(t0 - fabs(t0) * 1e-12, 0.01 * (1. - 1e-12));
+            t1 = t1 + fabs(t1) * 1e-12;
+            bool hit = t0 <= t1;
+            const double slack = 1e-12 * (t1 * (sU + sV) + (1. + t1) * (F.ru + F.rv)) + F.eps;
+            const double a0 = fabs(1. - t0), a1 = fabs(1. - t1);
+            const double lu = fmin(t0 * ulo - a0 * F.ru, t1 * ulo - a1 * F.ru) - slack;
+            const double hu = fmax(t0 * uhi + a0 * F.ru, t1 * uhi + a1 * F.ru) + slack;
+            const double lv = fmin(t0 * vlo - a0 * F.rv, t1 * vlo - a1 * F.rv) - slack;
+            const double hv = fmax(t0 * vhi + a0 * F.rv, t1 * vhi + a1 * F.rv) + slack;
+            hit = hit && cu - rp <= hu && cu + rp >= lu && cv - rp <= hv && cv + rp >= lv;
+            hit = hit || !(rp < 1e300) || !(fabs(cu) + fabs(cv) + fabs(cz) < 1e300);  // NaN / inf: keep
+            if (hit) {
+                const uint32_t id = k;
+                w0 = n == 0 ? id : w0, w1 = n == 1 ? (w1 & 0xffff0000u) | id : w1;
+                w1 = n == 2 ? (w1 & 0xffffu) | (id << 16) : w1;
+                w2 = n == 3 ? (w2 & 0xffff0000u) | id : w2, w2 = n == 4 ? (w2 & 0xffffu) | (id << 16) : w2;
+                w3 = n == 5 ? (w3 & 0xffff0000u) | id : w3, w3 = n == 6 ? (w3 & 0xffffu) | (id << 16) : w3;
+                ++n;
+            }
+        }
+        if (n <= kListMax) out = make_uint4(n | (w0 << 16), w1, w2, w3);
+    }
+    P.plist[t] = out;
+}
+
 // Phase 1, persistent form, with the heavy tail folded in. Every lane of a
 // cursor wave runs one pixel at a time and, when the pixel completes, takes the
 // next pixel of the shard from a global cursor (one atomic per wave per refill).
@@ -1498,11 +1619,12 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
 
     Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
     double seg_sa = 0.;  // sqrt(a) of the current segment (BVH hit), reused by the scatter
+    uint4 plst = no_list();  // the camera-ray candidate list of the lane's pixel's tile
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
             return bvh_hit<true>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x,
-                                 &seg_sa);
+                                 &seg_sa, plst);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -1588,6 +1710,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
                 uint32_t base = 0;
                 if (rank == 0) base = atomicAdd(KP(pix_cursor), static_cast<uint32_t>(__popcll(m)));
+#ifdef RTW_WALK_DIAG  // diagnostic build: device-scope atomics of the cursor loop
+                if (rank == 0) atomicAdd(&P.counters[16], 1ull);
+#endif
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
                 hotpix = ticket < P.hot_tickets;
@@ -1608,6 +1733,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     }
                     ps.rng = KP(seeds)[pix];
                     ps.k = 0;
+                    if (const uint4 *pls = KP(plist)) plst = pls[(lr >> KP(plist_thlog)) * KP(plist_tx) + (x >> 3)];
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
                     spec = false;
@@ -1746,6 +1872,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 if (kind != RTW_DIELECTRIC) {  // the bounce's attenuation row
                     if (ended) cr = M.a0 * 0., cg = M.a1 * 0., cb = M.a2 * 0.;  // att x black
                     else p.stk.push(static_cast<uint32_t>(best), KP(spill), stride, gid);
+#ifdef RTW_WALK_DIAG
+                    if (!ended && p.stk.n > kRegSlots) atomicAdd(&P.counters[18], 1ull);  // spill-level pushes
+#endif
                 }
                 p.ox = hx, p.oy = hy, p.oz = hz;
                 p.dx = ndx, p.dy = ndy, p.dz = ndz;
@@ -1779,6 +1908,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     const uint64_t dm = __ballot(done);
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
                         atomicAdd(KP(pixels_done), static_cast<uint32_t>(__popcll(dm)));
+#ifdef RTW_WALK_DIAG
+                    if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
+                        atomicAdd(&P.counters[17], 1ull);
+#endif
                 }
             }
             STAMP(7);  // 7: fold + pixel sum + decisions
@@ -2101,6 +2234,7 @@ struct rtw_session {
     uint32_t *d_park_flag = nullptr; // per park slot publish flags
     uint32_t *d_order = nullptr, *d_cost = nullptr, *d_cost_hist = nullptr;  // cost-ordered hand-out
     uint32_t *d_pcost = nullptr;
+    uint4 *d_plist = nullptr;        // camera-ray candidate lists, one per tile (<= one per pixel)
     uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
     size_t diag_bytes = 0, diag_n = 0;
     int n_cu = 0;
@@ -2447,15 +2581,16 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         dev_free(s->d_park);
         s->d_park = nullptr, s->park_cap = 0;
         dev_free(s->d_seeds), dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost);
-        dev_free(s->d_pcost);
+        dev_free(s->d_pcost), dev_free(s->d_plist);
         s->d_seeds = nullptr, s->d_park_flag = nullptr, s->d_order = nullptr, s->d_cost = nullptr;
-        s->d_pcost = nullptr;
+        s->d_pcost = nullptr, s->d_plist = nullptr;
         HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
         HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
         HIPCHECK(hipMalloc(&s->d_park_flag, npix_sh * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_order, npix_sh * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_cost, 2 * npix_sh * sizeof(uint32_t)));  // 2 words per 8x8 tile
         HIPCHECK(hipMalloc(&s->d_pcost, npix_sh * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_plist, npix_sh * sizeof(uint4)));
         s->park_cap = npix_sh;
     }
     P.park = s->d_park;
@@ -2549,6 +2684,44 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((seed_threads + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
+        // camera-ray candidate lists (rtw_primary_lists), BVH scenes: 8-pixel-wide
+        // tiles of 8 image rows' worth of the shard (a row shard's rows are row_step
+        // apart).
+        P.plist = nullptr;
+        // Opt-in (RTW_PLIST=1): measured 1.4 % slower at N=1 (profiles/r03_misc/
+        // ab_camera_ray_lists_REJECTED.log). Camera rays walk no shorter than others
+        // (5.46 visits vs 5.39), so the wave's walk -- the max over its lanes -- drops
+        // only 8.7 % without them (walk_diag_camera_rays.log), and the lists' exact
+        // tests, the fill and the list kernel eat that.
+        bool plist_on = false;
+        if (const char *e = std::getenv("RTW_PLIST")) plist_on = std::atoi(e) != 0;
+        plist_on = plist_on && mode == kBvh && P.max_depth > 0 && s->n_node > 0;
+        if (plist_on) {
+            PrimFrame F{};
+            auto cp3 = [](double *d, const rtw_vec3 &v) { d[0] = v.x, d[1] = v.y, d[2] = v.z; };
+            cp3(F.from, cam->look_from), cp3(F.u, cam->u), cp3(F.v, cam->v), cp3(F.w, cam->w);
+            auto dotv = [](const rtw_vec3 &a, const double *b) { return a.x * b[0] + a.y * b[1] + a.z * b[2]; };
+            const bool disk = cam->defocus_angle > 0.;
+            const double pad = 1. + 1e-9;
+            F.ru = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.u)) + std::fabs(dotv(cam->defocus_disk_v, F.u))) * pad : 0.;
+            F.rv = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.v)) + std::fabs(dotv(cam->defocus_disk_v, F.v))) * pad : 0.;
+            F.rz = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.w)) + std::fabs(dotv(cam->defocus_disk_v, F.w))) * pad : 0.;
+            auto nrm = [](const rtw_vec3 &v) { return std::fabs(v.x) + std::fabs(v.y) + std::fabs(v.z); };
+            F.eps = 1e-9 * (nrm(cam->look_from) + nrm(cam->pixel00) + (cam->img_width + 1.) * nrm(cam->pixel_delta_u) +
+                            (cam->img_height + 1.) * nrm(cam->pixel_delta_v) + F.ru + F.rv + F.rz + 1.);
+            F.tw = 8;
+            F.th = std::max(1u, 8u / std::max(1u, P.row_step));  // 8, 4, 2 or 1: a power of two
+            if (F.th & (F.th - 1u)) F.th = 1u;
+            F.tx = (P.W + F.tw - 1) / F.tw;
+            F.ty = (P.n_rows + F.th - 1) / F.th;
+            if (std::isfinite(F.eps) && static_cast<uint64_t>(F.tx) * F.ty <= npix) {
+                P.plist = s->d_plist;
+                P.plist_thlog = static_cast<uint32_t>(__builtin_ctz(F.th)), P.plist_tx = F.tx;
+                hipLaunchKernelGGL(rtw_primary_lists, dim3((F.tx * F.ty + kBlock - 1) / kBlock), dim3(kBlock), 0, st, P,
+                                   F);
+                HIPCHECK(hipGetLastError());
+            }
+        }
         // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
         // bottom-up, 0 row-major
         P.order_map = nullptr;
@@ -2836,8 +3009,9 @@ void collect(rtw_session *s) {
     HIPCHECK(hipMemcpy(c, s->d_counters, sizeof c, hipMemcpyDeviceToHost));
 #ifdef RTW_WALK_DIAG
     std::fprintf(stderr, "walk_diag: wave-iters %llu, sum max visits all %llu, without camera rays %llu, "
-                         "camera rays only %llu; camera-ray segments %llu, their visits %llu\n",
-                 c[1], c[11], c[12], c[13], c[14], c[15]);
+                         "camera rays only %llu; camera-ray segments %llu, their visits %llu; cursor atomics %llu, "
+                         "completion atomics %llu, spill-level pushes %llu\n",
+                 c[1], c[11], c[12], c[13], c[14], c[15], c[16], c[17], c[18]);
 #endif
     float ms = 0.f;
     HIPCHECK(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -3057,7 +3231,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
-    dev_free(s->d_pcost), dev_free(s->d_err);
+    dev_free(s->d_pcost), dev_free(s->d_plist), dev_free(s->d_err);
     dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);

@@ -201,6 +201,7 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0", "endgame_coopg16"),
     ("2", "0", "probe2"), ("2", "0.3", "probe3"),  # cost probe on one pixel per 2x2 / 3x3 block
     ("2", "0", "prepark"), ("2", "0", "drainprio0"),  # probe-hot pixels parked at once; drain at prio 0
+    ("2", "0", "plist1"), ("2", "0.3", "plist1"),  # camera rays take per-tile candidate lists (opt-in)
 ]
 
 
@@ -223,6 +224,7 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_PROBE_SUB", coop[5:] if coop.startswith("probe") else "1")
     monkeypatch.setenv("RTW_PREPARK", "4" if coop == "prepark" else "0")
     monkeypatch.setenv("RTW_DRAIN_PRIO", "0" if coop == "drainprio0" else "1")
+    monkeypatch.setenv("RTW_PLIST", "1" if coop == "plist1" else "0")
     if coop == "endgame_coopg16":
         monkeypatch.setenv("RTW_COOPG", "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
@@ -507,3 +509,33 @@ def test_shutdown_frees_and_recreates_sessions():
     fb, _ = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 2, SEED, devices=[0, 0, 0, 0])
     assert np.array_equal(fb, ref)
     rtw.shutdown()
+
+
+@pytest.mark.parametrize("plist", ["1", "0"])
+def test_camera_ray_lists_on_frustum_edges(monkeypatch, plist):
+    """Camera rays take their tile's candidate list (rtw_primary_lists) instead of the
+    walk. A scene built to sit on the lists' bounds: spheres tangent to pixel and
+    tile frusta, grazing the defocus cone, straddling the focus plane, behind and
+    around the camera, a camera inside a sphere, and a sphere cluster wider than a
+    list (no list: walk). Bit-exact with lists on and off."""
+    monkeypatch.setenv("RTW_PLIST", plist)
+    rng = np.random.default_rng(23)
+    world = rtw.SceneBuilder()
+    lam = rtw.Lambertian((0.6, 0.5, 0.4))
+    world.add(rtw.Sphere.new_world_obj(0., -1000., 0., 1000., lam))
+    for _ in range(220):
+        c = rng.uniform(-3, 3, 3)
+        c[2] = -abs(c[2]) * 2 - 0.5
+        r = float(10 ** rng.uniform(-3, -0.5))
+        m = lam if rng.random() < 0.4 else rtw.Metal((0.9, 0.8, 0.7), 0.2) if rng.random() < 0.5 else rtw.Dielectric(1.5)
+        world.add(rtw.Sphere.new_world_obj(*map(float, c), r, m))
+    for k in range(12):  # a tight cluster: more candidates than a list holds
+        world.add(rtw.Sphere.new_world_obj(0.01 * k, 0.2, -2.0, 0.05, lam))
+    world.add(rtw.Sphere.new_world_obj(0., 0.3, 1.2, 0.3, lam))    # behind the camera
+    world.add(rtw.Sphere.new_world_obj(0., 0.4, 1., 0.6, rtw.Dielectric(1.5)))  # the camera inside glass
+    sph, n, mt, nm = world.build().flatten()
+    for cam in (rtw.Camera.new(30, 48, 12, 1.0, 50.0, (0., 0.4, 1.), (0., 0.1, -2.), (0., 1., 0.), 4.0, 3.0),
+                rtw.Camera.new(31, 29, 12, 1.0, 90.0, (0., 0.4, 1.), (0.3, 0.2, -2.), (0., 1., 0.), 0.0, 1.0)):
+        fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, 2, 404)
+        ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, 404)
+        assert_same(fb, ref, st, seg)
