@@ -142,7 +142,7 @@ def read_counters(d):
     return out
 
 
-def pmc_live(a, timeout_s=150):
+def pmc_live(a, timeout_s=75):
     """Separate rocprofv3 --pmc passes over a one-frame child (no tracing in the same
     run). Returns {pass: {kernel: {counter: value per dispatch}}} or None."""
     exe = shutil.which("rocprofv3")

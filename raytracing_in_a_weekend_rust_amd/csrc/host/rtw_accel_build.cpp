@@ -219,8 +219,16 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     }
     if (out.always.size() > kMaxAlways) return false;
     const uint32_t m = static_cast<uint32_t>(rest.size());
-    out.leaves.assign(8 * static_cast<size_t>(n), 0.f);  // indexed by sphere ("always" slots unused)
+    // indexed by sphere; the walk never reaches an "always" slot, but every slot holds
+    // its sphere's pass-1 record: the drain groups read them as their filter records
+    out.leaves.assign(8 * static_cast<size_t>(n), 0.f);
     out.n_leaf = n;
+    for (uint32_t i : out.always) {
+        float *L = &out.leaves[8 * static_cast<size_t>(i)];
+        L[0] = static_cast<float>(centers[3 * i]), L[1] = static_cast<float>(centers[3 * i + 1]);
+        L[2] = static_cast<float>(centers[3 * i + 2]), L[3] = r2p[i];
+        L[5] = as_f32(i);
+    }
     if (m == 0) return true;
     Builder b{centers, radii, r2p, rest, &out};
     b.median = std::getenv("RTW_BVH_MEDIAN") != nullptr;

@@ -56,7 +56,10 @@ constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 // 768 threads = 3 waves per SIMD at the BVH kernel's ~150 VGPRs. (A 1024-thread
 // build fits 128 VGPRs with the per-lane LDS areas and few spills, but measured
 // slower: bulk throughput no better, drain groups slower.)
-constexpr int kPBlock = 768;
+#ifndef RTW_PBLOCK
+#define RTW_PBLOCK 768  // diagnostic builds: -DRTW_PBLOCK=512 (2 waves per SIMD)
+#endif
+constexpr int kPBlock = RTW_PBLOCK;
 constexpr int kTile = 16;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
@@ -113,12 +116,13 @@ struct U128 {
 typedef __attribute__((address_space(1))) uint32_t gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-// Per-sphere shading record (48 B): the sphere's radius and its material row
-// flattened (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric);
-// nbr = the sphere's inside-cut list (offset << 8 | count into KParams::nbr, or
-// rtw_accel::kNbrNone; rtw_accel.h "Inside cut").
+// Per-sphere shading record (40 B): the sphere's material row flattened
+// (materials.rs:11-111): albedo, p = fuzz (Metal) or ir (Dielectric); nbr = the
+// sphere's inside-cut list (offset << 8 | count into KParams::nbr, or
+// rtw_accel::kNbrNone; rtw_accel.h "Inside cut"). The radius is the sphere
+// record's w (KParams::sph).
 struct ShadeRec {
-    double r, a0, a1, a2, p;
+    double a0, a1, a2, p;
     uint32_t kind, nbr;
 };
 
@@ -153,7 +157,8 @@ struct KParams {
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
                                 // segments is parked before its first sample (0: off)
     uint64_t seed_lo, seed_hi;
-    const double4 *sph;         // {cx, cy, cz, r*r} f64 (the reference's values)
+    const double4 *sph;         // {cx, cy, cz, r} f64 (the reference's values; r*r formed at each
+                                // use, as sphere.rs:49 does)
     const float4 *filt;         // {cx, cy, cz, R2'} f32, padded to kChunk (pass 1 only)
     const float4 *nodes;        // BVH inner nodes, 2 float4 each (rtw_accel.h)
     const float4 *leaves;       // BVH leaves, 2 float4 each
@@ -392,7 +397,15 @@ struct SceneView {
     const ShadeRec *shd;
     const float4 *nodes, *leaves;
     const uint16_t *nbr;
+    float4 *end;  // first LDS float4 after the staged scene (kLds), else nullptr
 };
+// Shading records in LDS (default) or read from HBM through the caches
+// (RTW_SHADE_GLOBAL builds: 23 KB of LDS freed for more lanes per CU)
+#ifdef RTW_SHADE_GLOBAL
+constexpr size_t kShadeLds = 0;
+#else
+constexpr size_t kShadeLds = sizeof(ShadeRec);
+#endif
 // inside-cut list entries (u16) in float4 units
 __host__ __device__ constexpr uint32_t nbr_f4(uint32_t n_nbr) { return (n_nbr + 7u) / 8u; }
 // BVH nodes in float4 units, padded to 32 B (the double4 records after them)
@@ -402,7 +415,7 @@ __host__ __device__ constexpr uint32_t node_area_f4(uint32_t n_node) { return (r
 // sph | [n] ShadeRec | (BVH) inside-cut lists (padded to float4)
 __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uint32_t n_leaf, bool bvh,
                                                 uint32_t n_nbr = 0) {
-    return static_cast<size_t>(n) * (sizeof(double4) + sizeof(ShadeRec)) +
+    return static_cast<size_t>(n) * sizeof(double4) + ((static_cast<size_t>(n) * kShadeLds + 15) & ~size_t(15)) +
            (bvh ? (static_cast<size_t>(node_area_f4(n_node)) + 2 * static_cast<size_t>(n_leaf) + nbr_f4(n_nbr)) *
                       sizeof(float4)
                 : 0);
@@ -590,7 +603,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
     const double4 S = sph[best];
     const ShadeRec M = shd[best];
-    const double r = M.r;
+    const double r = S.w;
     const double px = p.dx * bt + p.ox, py = p.dy * bt + p.oy, pz = p.dz * bt + p.oz;
     double nx = px - S.x, ny = py - S.y, nz = pz - S.z;
     rtw_num::div3(nx, ny, nz, r);  // (p - c) / r
@@ -815,7 +828,7 @@ __device__ __forceinline__ void exact_test(const double4 *__restrict__ sph, uint
                                            double a, int &best, double &bt) {
     const double4 S = sph[i];
     double t;
-    if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t) &&
+    if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w, t) &&
         rtw_accel::better(t, i, bt, best)) {
         bt = t;
         best = static_cast<int>(i);
@@ -908,7 +921,9 @@ constexpr uint32_t kListMax = 7;
 constexpr uint32_t kListNone = 0xffffu;
 __device__ __forceinline__ uint4 no_list() { return make_uint4(kListNone, 0u, 0u, 0u); }
 
-template <bool kLdsStack = false>
+// kStride: the LDS scratch column stride (the workgroup size; a constant, so the
+// walk's pointer steps are immediates and hold no register)
+template <bool kLdsStack = false, uint32_t kStride = 0>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
@@ -944,7 +959,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
 #ifdef RTW_SELF_SKIP  // opt-in: measured +0.8 % (the wave's candidate loop is set by real candidates)
             {  // the sphere the segment leaves is no candidate (rtw_accel.h self_skip)
                 const double4 S = sph[prev >= 0 ? prev : 0];
-                wr.skip = rtw_accel::self_skip(prev, ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w);
+                wr.skip = rtw_accel::self_skip(prev, ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w);
             }
 #endif
             auto run = [&](auto &ws) {
@@ -971,7 +986,8 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
             };
             bool walked;
             if constexpr (kLdsStack) {
-                rtw_accel::LdsScratch ws(scol, blockDim.x);
+                static_assert(!kLdsStack || kStride > 0, "LDS scratch needs its stride");
+                rtw_accel::LdsScratch ws(scol, kStride);
                 walked = run(ws);
             } else {
                 rtw_accel::ArrayScratch ws;
@@ -1017,7 +1033,7 @@ __device__ __forceinline__ void flush_tally(const KParams &P, const Tally &tl, b
 
 template <bool kLds, int kMode>
 __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds) {
-    SceneView v{P.sph, P.shade, P.nodes, P.leaves, P.nbr};
+    SceneView v{P.sph, P.shade, P.nodes, P.leaves, P.nbr, nullptr};
     if (kLds) {
         const uint32_t n = P.n_sph;
         double4 *ld = lds;
@@ -1031,16 +1047,22 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
             ld = reinterpret_cast<double4 *>(lf + na + nl);
         }
         for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ld[i] = P.sph[i];
-        ShadeRec *ls = reinterpret_cast<ShadeRec *>(ld + n);
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
+        char *end = reinterpret_cast<char *>(ld + n);
+        if constexpr (kShadeLds != 0) {
+            ShadeRec *ls = reinterpret_cast<ShadeRec *>(end);
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ls[i] = P.shade[i];
+            v.shd = ls;
+            end += (static_cast<size_t>(n) * sizeof(ShadeRec) + 15) & ~size_t(15);
+        }
         if (kMode == kBvh) {
-            uint16_t *lnb = reinterpret_cast<uint16_t *>(ls + n);
+            uint16_t *lnb = reinterpret_cast<uint16_t *>(end);
             for (uint32_t i = threadIdx.x; i < P.n_nbr; i += blockDim.x) lnb[i] = P.nbr[i];
             v.nbr = lnb;
+            end += static_cast<size_t>(nbr_f4(P.n_nbr)) * sizeof(float4);
         }
         __syncthreads();
         v.sph = ld;
-        v.shd = ls;
+        v.end = reinterpret_cast<float4 *>(end);
     }
     return v;
 }
@@ -1226,7 +1248,7 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
     if (info == rtw_accel::kNbrNone) return false;
     const double4 S = sph[prev];
     double t;
-    if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w, t)) return false;
+    if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w, t)) return false;
     const uint32_t n = info & 0xffu;  // group-uniform
     if (sub == 0) tl.inside += 1u, tl.ntest += 1u + n;
     best = prev, bt = t;
@@ -1238,7 +1260,7 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
         asm volatile("" : "+v"(e));
         const uint32_t i = nbr[e];
         const double4 T = sph[i];
-        if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w, t) &&
+        if (rtw_accel::sphere_hit_f64(ox, oy, oz, dx, dy, dz, a, T.x, T.y, T.z, T.w * T.w, t) &&
             rtw_accel::better(t, i, bt, best))
             bt = t, best = static_cast<int>(i);
     }
@@ -1257,7 +1279,7 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
 // Returns the pixel's segments on the group's first lane (0 on the others).
 template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
-                                               const float4 *__restrict__ filt, const Parked &q,
+                                               const float4 *__restrict__ filt, uint32_t fsh, const Parked &q,
                                                uint64_t col, Tally &tl, Stamps &stp) {
 #ifdef RTW_DIAG_NO_COOP  // register-pressure experiment only: the cursor path alone
     return 0;
@@ -1273,12 +1295,15 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
     // scenes of up to kCoopRegRec * kG spheres: the lane's pass-1 records live in
     // registers for the whole pixel (no LDS round trip on the serial chain)
-    constexpr uint32_t kCoopRegRec = 8;
-    const bool rec_in_regs = n <= kCoopRegRec * kG;
+#ifndef RTW_COOP_REGREC
+#define RTW_COOP_REGREC 8  // 0: records always from LDS (register-pressure experiments)
+#endif
+    constexpr uint32_t kCoopRegRec = RTW_COOP_REGREC > 0 ? RTW_COOP_REGREC : 1;
+    const bool rec_in_regs = RTW_COOP_REGREC > 0 && n <= kCoopRegRec * kG;
     float4 rr[kCoopRegRec];
     if (rec_in_regs) {
 #pragma unroll
-        for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u)];
+        for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u) << fsh];
     }
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
@@ -1315,7 +1340,7 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
 #pragma unroll 8
             for (uint32_t j = 0; j < jn; ++j) {
                 const uint32_t i = base + sub + j * kG;
-                const float4 rec = filt[min(i, n - 1u)];
+                const float4 rec = filt[min(i, n - 1u) << fsh];
                 mask |= static_cast<uint32_t>((i < n) & (!g.fast | g.pass(rec))) << j;
             }
             STAMP(5);  // coop: segment setup + filter
@@ -1422,7 +1447,7 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
                 ++segs;
                 const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
                 double bt = 0.;
-                const int best = bvh_hit<kLds>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
+                const int best = bvh_hit<kLds, kProbeBlock>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
                 if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
                 double cr, cg, cb;
                 shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
@@ -1548,7 +1573,7 @@ __global__ __launch_bounds__(kBlock) void rtw_primary_lists(const KParams P, con
                 continue;
             }
             const double4 S = P.sph[k];
-            const double r = fabs(P.shade[k].r);
+            const double r = fabs(S.w);
             const double dx = S.x - F.from[0], dy = S.y - F.from[1], dz = S.z - F.from[2];
             const double cu = dx * F.u[0] + dy * F.u[1] + dz * F.u[2];
             const double cv = dx * F.v[0] + dy * F.v[1] + dz * F.v[2];
@@ -1598,9 +1623,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
     // pass-1 records after the scene view: after the inside-cut lists (BVH) or the
     // shading records
-    float4 *filt_lds = reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph);
-    if (kMode == kBvh) filt_lds += nbr_f4(P.n_nbr);
-    const float4 *filt = stage_filt<kLds>(P, filt_lds);
+    // BVH scenes in LDS: the leaves (indexed by sphere, every sphere's record, rtw_accel.h)
+    // are the pass-1 records, at a stride of 2 float4; else staged after the scene
+    constexpr bool kLeafFilt = kLds && kMode == kBvh;
+    constexpr uint32_t fsh = kLeafFilt ? 1u : 0u;
+    const float4 *filt = kLeafFilt ? sv.leaves : stage_filt<kLds>(P, sv.end);
     // per-lane LDS areas (lane_lds_bytes): the pixel's running sum (3 f64 columns,
     // read and written once per sample) and the BVH walk scratch (kScratch u16
     // columns) -- state that would otherwise hold ~12 VGPRs through the walk
@@ -1623,7 +1650,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x,
+            return bvh_hit<true, kThreads>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x,
                                  &seg_sa, plst);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
@@ -1683,7 +1710,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+            cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
             if (sub == 0) atomicAdd(P.park_processed, 1u);
         }
         tl.seg += cseg;
@@ -1733,7 +1760,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     }
                     ps.rng = KP(seeds)[pix];
                     ps.k = 0;
+#ifndef RTW_NO_PLIST
                     if (const uint4 *pls = KP(plist)) plst = pls[(lr >> KP(plist_thlog)) * KP(plist_tx) + (x >> 3)];
+#endif
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
                     spec = false;
@@ -1836,7 +1865,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 // HitRecord: point = dir*t + orig, outward = (p - c)/r, face_normal
                 const double4 S = sph[best];
                 const ShadeRec M = sv.shd[best];
-                const double r = M.r;
+                const double r = S.w;
                 const double hx = p.dx * bt + p.ox, hy = p.dy * bt + p.oy, hz = p.dz * bt + p.oz;
                 double nx = hx - S.x, ny = hy - S.y, nz = hz - S.z;
                 rtw_num::div3(nx, ny, nz, r);  // (p - c) / r
@@ -2098,7 +2127,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cseg += coop_pixel<kCoopG>(P, sv, filt, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
         if (sub == 0) atomicAdd(P.park_processed, 1u);
     }
     tl.seg += cseg;
@@ -2114,8 +2143,7 @@ __global__ __launch_bounds__(kBlock) void rtw_park_leftover(const KParams P) {
     if (*P.park_processed >= *P.park_count) return;  // block-uniform
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
-    const float4 *filt =
-        stage_filt<kLds>(P, reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph));
+    const float4 *filt = stage_filt<kLds>(P, sv.end);
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const int gl = static_cast<int>(threadIdx.x & 63u & ~(kG - 1u));
     Tally tl;
@@ -2135,7 +2163,7 @@ __global__ __launch_bounds__(kBlock) void rtw_park_leftover(const KParams P) {
         const Parked q = P.park[item];
         // spill columns: region B, column = slot (the persistent kernel's groups
         // used group-base columns; a kernel boundary separates the two uses)
-        seg += coop_pixel<kG>(P, sv, filt, q, item, tl, stp);
+        seg += coop_pixel<kG>(P, sv, filt, 0u, q, item, tl, stp);
         if (sub == 0) {
             atomicAdd(&P.counters[10], 1ull);
             atomicAdd(P.park_processed, 1u);
@@ -2150,8 +2178,7 @@ template <bool kLds, uint32_t kG>
 __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
-    const float4 *filt =
-        stage_filt<kLds>(P, reinterpret_cast<float4 *>(const_cast<ShadeRec *>(sv.shd) + P.n_sph));
+    const float4 *filt = stage_filt<kLds>(P, sv.end);
     const uint32_t sub = threadIdx.x & (kG - 1u);
     Tally tl;
     Stamps stp;
@@ -2162,7 +2189,7 @@ __global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
         item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
         if (item >= *P.park_count) break;
         const Parked q = P.park[item];
-        seg += coop_pixel<kG>(P, sv, filt, q, item, tl, stp);
+        seg += coop_pixel<kG>(P, sv, filt, 0u, q, item, tl, stp);
     }
 #ifdef RTW_STAMPS
     if ((threadIdx.x & 63u) == 0) {  // diagnostic: per-wave rows after the tile kernel's
@@ -2344,7 +2371,7 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         const double rad = sp[i].radius;
         const double rr = rad * rad;  // sphere.rs:49 `self.radius * self.radius`
         const double *c = sp[i].center;
-        a[i] = make_double4(c[0], c[1], c[2], rr);
+        a[i] = make_double4(c[0], c[1], c[2], rad);  // r*r formed at each use (sphere.rs:49)
         // R2' >= r*r + K (m_c^2 + r*r/2), m_c = max |c_i|, rounded up to f32; +inf
         // (always tested exactly) outside the guard or for non-finite input.
         const float r2p = rtw_accel::filter_r2p(c, rr);
@@ -2353,7 +2380,6 @@ void set_scene(rtw_session *s, const rtw_sphere *sp, uint32_t n, const rtw_mater
         // the sphere's material row, flattened next to its radius
         const rtw_material &M = m[sp[i].mat];
         ShadeRec &R = sh[i];
-        R.r = rad;
         R.a0 = M.albedo[0], R.a1 = M.albedo[1], R.a2 = M.albedo[2];
         R.p = M.kind == RTW_METAL ? M.fuzz : M.kind == RTW_DIELECTRIC ? M.ir : 0.;
         R.kind = M.kind, R.nbr = rtw_accel::kNbrNone;
@@ -2667,7 +2693,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     bool persist = true;
     if (const char *e = std::getenv("RTW_PERSIST")) persist = std::atoi(e) != 0;
     size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh, P.n_nbr);
-    if (persist) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);  // pass-1 records (coop groups)
+    // pass-1 records for the coop groups (BVH scenes read them from the leaves)
+    if (persist && mode != kBvh) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);
     const bool use_lds = lds <= kLdsCap;
     if (!use_lds) lds = 0;
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
