@@ -6,15 +6,18 @@ HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 # xnack- : the pool runs without XNACK (no page-fault retry), and code built for it is
 # free of the xnack-any constraints: 127.9 -> 127.5 ms per image, 8-round A/B
-# (profiles/r02_misc/ab_xnack_off.log). Such a code object does not load on a gfx950
-# running with XNACK enabled: `make ARCH=gfx950` builds the portable (xnack-any) one.
-# rtw_version() names the target feature the library was built for.
-ARCH ?= gfx950:xnack-
+# (profiles/r02_misc/ab_xnack_off.log). A gfx950 running with XNACK enabled loads the
+# xnack+ code object built beside it (one fat binary, the runtime picks the one that
+# matches the device's mode); `make ARCH=gfx950` builds a single portable (xnack-any)
+# object instead. rtw_version() names the target features the library carries.
+ARCH ?= gfx950:xnack- gfx950:xnack+
 PKG := raytracing_in_a_weekend_rust_amd
 SRC := $(PKG)/csrc
 OUT := $(PKG)/_lib
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+ARCHFLAGS := $(foreach a,$(ARCH),--offload-arch=$(a))
+HIPFLAGS_1 := -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
             -Wall -Iinclude -I$(SRC) -I$(SRC)/host $(EXTRA)
+HIPFLAGS := $(ARCHFLAGS) $(HIPFLAGS_1)
 CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra \
             -Iinclude -I$(SRC)/host -D__HIP_PLATFORM_AMD__
 # Build id: hash of every library source and the device flags. rtw_build_id()
@@ -60,7 +63,7 @@ $(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_h
 	$(CXX) $(CXXFLAGS) -I$(OUT) -c $< -o $@
 
 $(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
+	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
 
 $(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN' -lpthread
@@ -73,11 +76,11 @@ stamps: $(OUT)/librtw_stamps.so
 $(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
 	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
 $(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
+	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
 asm: $(SRC)/rtw_render.hip
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S -o build/rtw_render.s $<
+	$(HIPCC) --offload-arch=$(firstword $(ARCH)) $(HIPFLAGS_1) --cuda-device-only -S -o build/rtw_render.s $<
 
 # A/B variant of the library (tools/libab.py): make ablib NAME=x EXTRA=-DFOO -> ab/x/librtw.so
 ablib:

@@ -29,6 +29,7 @@ def main():
     stream = torch.cuda.current_stream()
     fb = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0")
     base_env = dict(os.environ)
+    ref = {}  # the first setting's image per shard: every other setting must match it bit for bit
     for st in settings:
         os.environ.clear()
         os.environ.update(base_env)
@@ -49,7 +50,9 @@ def main():
                 ms = e0.elapsed_time(e1)
                 best = ms if best is None else min(best, ms)
             s = sess.stats()
-            row.append(f"{N}:{r} {best:7.1f} ms (parked {s.parked_pixels}, inside {s.inside_segments / max(1, s.segments):.3f}, trap {s.trap_segments / max(1, s.segments):.4f})")
+            img = fb[:rows].clone()
+            same = ref.setdefault((N, r), img).equal(img)
+            row.append(f"{N}:{r} {best:7.1f} ms{'' if same else ' IMAGE DIFFERS'} (parked {s.parked_pixels}, inside {s.inside_segments / max(1, s.segments):.3f}, trap {s.trap_segments / max(1, s.segments):.4f})")
         print(f"[{st or 'defaults'}] " + " | ".join(row), flush=True)
     sess.close()
 
