@@ -6,11 +6,12 @@ HIPCC ?= /opt/rocm/bin/hipcc
 CXX ?= g++
 # xnack- : the pool runs without XNACK (no page-fault retry), and code built for it is
 # free of the xnack-any constraints: 127.9 -> 127.5 ms per image, 8-round A/B
-# (profiles/r02_misc/ab_xnack_off.log). A gfx950 running with XNACK enabled loads the
-# xnack+ code object built beside it (one fat binary, the runtime picks the one that
-# matches the device's mode); `make ARCH=gfx950` builds a single portable (xnack-any)
-# object instead. rtw_version() names the target features the library carries.
-ARCH ?= gfx950:xnack- gfx950:xnack+
+# (profiles/r02_misc/ab_xnack_off.log). Such a code object does not load on a gfx950
+# running with XNACK enabled: `make ARCH=gfx950` builds the portable (xnack-any) one.
+# (A fat binary with an xnack+ object beside it is not an option here: the GPU pool
+# refuses any tree that carries xnack+ code.) ARCH may list several targets;
+# rtw_version() names the target features the library carries.
+ARCH ?= gfx950:xnack-
 PKG := raytracing_in_a_weekend_rust_amd
 SRC := $(PKG)/csrc
 OUT := $(PKG)/_lib

@@ -318,6 +318,16 @@ class Session:
         check(lib.rtw_session_diag(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
         return out[:2 * n_pixels].reshape(n_pixels, 2), int(out[2 * n_pixels])
 
+    def diag_events(self, n_pixels: int):
+        """RTW_DIAG=2 renders: per pixel (segments, completion, hand-out, first park,
+        first drain claim) as raw 100 MHz clock words (0: never), and the launch start."""
+        import numpy as np
+        out = np.zeros(5 * n_pixels + 4, dtype=np.uint32)
+        check(lib.rtw_session_diag(self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), out.size))
+        rec = out[:2 * n_pixels].reshape(n_pixels, 2)
+        ev = out[2 * n_pixels + 4:].reshape(n_pixels, 3)
+        return np.concatenate([rec, ev], axis=1), int(out[2 * n_pixels])
+
     def close(self):
         if self.h:
             lib.rtw_session_destroy(self.h)

@@ -179,6 +179,7 @@ struct KParams {
     uint32_t *park_cursor;
     U128 *seeds;                // per-pixel RNG children (persistent phase 1)
     uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
+    uint32_t diag_ev;           // RTW_DIAG=2: then per pixel {hand-out, first park, first claim} clocks
     uint32_t *order_map;        // hand-out order of the persistent kernel (pixel per ticket) or null
     uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base;
                                 // then per tile: its hot pixels
@@ -1158,6 +1159,12 @@ __global__ __launch_bounds__(kBlock) void rtw_seed_pixels(const KParams P) {
 // write-through (sc1) by 8-byte atomic stores, then a drain, then the flag
 // (cdna_hip_programming.md Guideline 16, recipe R1); consumers poll the flag
 // relaxed and load the entry by sc1 loads (no stale copy of a reused slot).
+// RTW_DIAG=2: the first time event k (0 hand-out, 1 park, 2 drain claim) happened to pixel pix
+__device__ __forceinline__ void diag_event(const KParams &P, uint64_t npix, uint64_t pix, uint32_t k) {
+    uint32_t *d = KP(diag);
+    if (d && KP(diag_ev))
+        atomicCAS(d + 2 * npix + 4 + 3 * pix + k, 0u, static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) | 1u);
+}
 __device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
     return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1293,6 +1300,7 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     ps.k = q.k;
     ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
     const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
+    if (sub == 0) diag_event(P, static_cast<uint64_t>(P.n_rows) * P.W, pix, 2);
     // scenes of up to kCoopRegRec * kG spheres: the lane's pass-1 records live in
     // registers for the whole pixel (no LDS round trip on the serial chain)
 #ifndef RTW_COOP_REGREC
@@ -1760,6 +1768,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     }
                     ps.rng = KP(seeds)[pix];
                     ps.k = 0;
+                    diag_event(P, npix, pix, 0);
 #ifndef RTW_NO_PLIST
                     if (const uint4 *pls = KP(plist)) plst = pls[(lr >> KP(plist_thlog)) * KP(plist_tx) + (x >> 3)];
 #endif
@@ -1772,6 +1781,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     } else if (P.prepark && order_map && KP(pcost)[pix] >= P.prepark) {
                         // a long serial chain by the probe's estimate: to a drain wave
                         // from its first sample
+                        diag_event(P, npix, pix, 1);
                         Parked q;
                         q.x = x, q.lr = lr, q.k = 0, q._pad = 0;
                         q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
@@ -2035,6 +2045,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     write_pixel(P, x, lr, ps, false);
                     need = true;
                 } else if (park) {  // park at the sample boundary
+                    diag_event(P, npix, pix, 1);
                     ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
                     Parked q;
                     q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
@@ -2662,9 +2673,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
 #endif
     P.counters = s->d_counters;
     P.diag = nullptr;
+    P.diag_ev = 0;
     if (const char *e = std::getenv("RTW_DIAG")) {
         if (std::atoi(e) != 0) {
-            const size_t need = (static_cast<size_t>(sh.n_rows) * cam->img_width * 2 + 4) * sizeof(uint32_t);
+            // RTW_DIAG=2: also per pixel {hand-out, first park, first drain claim} clocks
+            // after the {segments, completion} records
+            const size_t per = std::atoi(e) >= 2 ? 5u : 2u;
+            const size_t need = (static_cast<size_t>(sh.n_rows) * cam->img_width * per + 4) * sizeof(uint32_t);
             if (need > s->diag_bytes) {
                 HIPCHECK(hipSetDevice(s->device));
                 HIPCHECK(hipDeviceSynchronize());
@@ -2675,6 +2690,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             }
             HIPCHECK(hipMemsetAsync(s->d_diag, 0, need, stream));
             P.diag = s->d_diag;
+            P.diag_ev = per == 5u ? 1u : 0u;
             s->diag_n = need / sizeof(uint32_t);
         }
     }
