@@ -74,6 +74,9 @@ constexpr double kBudgetX = 14.0;
 // better than a fixed 768 (38.1 -> 36.1 ms; 1026 -> 864 ms per rank of 8 at 4096x2304)
 constexpr double kTailSegsPerSample = 768. / 529.;
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
+constexpr uint32_t kHeavyPerBlockFull = 6;  // ... in a shard of about one pixel per lane
+constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 samples) that park a
+                                            // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
@@ -1253,10 +1256,61 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
     if (prev < 0) return false;
     const uint32_t info = shd[prev].nbr;
     if (info == rtw_accel::kNbrNone) return false;
+    const uint32_t n = info & 0xffu;  // group-uniform, <= kMaxNbr < 16
+#ifndef RTW_INSIDE_SERIAL  // A/B: -DRTW_INSIDE_SERIAL tests S first, then the list
+    // One pass for S and its list, side by side on the group's first n + 1 lanes (the
+    // serial chain pays one sphere test instead of two in a row): lane j < n tests list
+    // entry j as Sphere::hit does, lane n tests S as inside_far does -- the same
+    // operations in the same order as those two functions, both roots formed -- then
+    // S's verdict is read from lane n and the (t, index) minimum of lanes 0..15 (one
+    // DPP row) is the group's. The candidates and the minimum are those of the serial
+    // form, so the result is too.
+    static_assert(rtw_accel::kMaxNbr < 16u, "the list and S fit one DPP row");
+    {
+        uint32_t i = static_cast<uint32_t>(prev);
+        if (sub < n) {
+            uint32_t e = (info >> 8) + sub;
+            asm volatile("" : "+v"(e));  // formed here (see below)
+            i = nbr[e];
+        }
+        const double4 T = sph[i];
+        const double ocx = ox - T.x, ocy = oy - T.y, ocz = oz - T.z;
+        const double rr = T.w * T.w;
+        const double hb = ocx * dx + ocy * dy + ocz * dz;
+        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rr;
+        const double disc = hb * hb - a * c;
+        const double sq = __builtin_sqrt(disc);
+        const double tn = (-sq - hb) / a, tf = (sq - hb) / a;
+        // lane n (S): inside_far's tests; lanes < n: sphere_hit_f64's
+        const bool s_ok = (c <= 3. * rr) && !(hb >= 0. && c >= 0.) && disc >= 0. && !(tn >= 0.01) && tf >= 0.01;
+        int okn;
+        if constexpr (kG == 64) {
+            okn = __builtin_amdgcn_readlane(static_cast<int>(s_ok), __builtin_amdgcn_readfirstlane(static_cast<int>(n)));
+        } else {
+            okn = __shfl(static_cast<int>(s_ok), static_cast<int>(n + (threadIdx.x & 63u & ~(kG - 1u))));
+        }
+        if (!okn) return false;
+        if (sub == 0) tl.inside += 1u, tl.ntest += 1u + n;
+        const double t = tn >= 0.01 ? tn : tf;
+        const bool cand = sub < n ? (disc >= 0. && t >= 0.01) : sub == n;
+        bt = sub == n ? tf : t;
+        best = cand ? static_cast<int>(i) : -1;
+        dpp_min_step<0xB1>(bt, best);   // quad_perm [1,0,3,2]
+        dpp_min_step<0x4E>(bt, best);   // quad_perm [2,3,0,1]
+        dpp_min_step<0x141>(bt, best);  // row_half_mirror
+        dpp_min_step<0x140>(bt, best);  // row_mirror
+        if (kG > 16) {  // every lane of the group takes row 0's result
+            const int src = static_cast<int>(threadIdx.x & 63u & ~(kG - 1u));
+            best = __builtin_amdgcn_readlane(best, src);
+            bt = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(bt), src),
+                                  __builtin_amdgcn_readlane(__double2loint(bt), src));
+        }
+        return true;
+    }
+#endif
     const double4 S = sph[prev];
     double t;
     if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w, t)) return false;
-    const uint32_t n = info & 0xffu;  // group-uniform
     if (sub == 0) tl.inside += 1u, tl.ntest += 1u + n;
     best = prev, bt = t;
     if (n == 0) return true;
@@ -2828,12 +2882,16 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // N=1 they are worth 15 % (1: 152 ms, 2: 128 ms; profiles/r03_drain1).
         const uint32_t wpb = static_cast<uint32_t>(pblock) / 64u;
         const bool small_shard = npix < static_cast<uint64_t>(grid_p) * (wpb - kHeavyPerBlock) * 64u;
-        // A shard of about one pixel per lane (N=4 of the bench image) takes a third
-        // priority wave: its medium chains all start at once and the drain has more to
-        // take (rank 70.2 -> 66-69 ms; N=1, 2, 8 lose with it: profiles/r03_misc/
-        // knobs_heavy_rate_endgame.log, knobs_hot_prio_endgame.log)
+        // A shard of about one pixel per lane (N=4 of the bench image) takes half its
+        // waves as priority waves: every pixel starts at once, a cursor lane of a full
+        // wave advances a segment every ~20 us, and the chains of more than ~4
+        // segments per sample must move to drains early, so the drain needs the waves
+        // (rank 67-68 -> 61.4-61.7 ms with the parking rules below; 3 waves: 66-69 ms;
+        // N=1, 2, 8 lose with more: profiles/r03_misc/knobs_small_shard_parking.log,
+        // knobs_heavy_rate_endgame.log)
         const double fill = static_cast<double>(npix) / (static_cast<double>(grid_p) * pblock);
-        uint32_t heavy = fill >= 0.75 && fill < 1.5 ? kHeavyPerBlock + 1u : kHeavyPerBlock;
+        const bool small_fill = fill < 1.5;  // strong scaling at N >= 4 of the bench image
+        uint32_t heavy = fill >= 0.75 && small_fill ? kHeavyPerBlockFull : kHeavyPerBlock;
         if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
@@ -2852,7 +2910,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
                                   : 0xffffffffu;
         // waves that signal the end of their cursor loop: priority waves too when they join
         P.n_cursor_waves = P.join_at != 0xffffffffu ? grid_p * wpb : grid_p * (wpb - heavy);
-        P.rate_k = 16, P.rate_x = 16;
+        // Park rules. Full images: after 16 samples above 16 segments per sample. Small
+        // shards (spare or half the waves drain): above 12, and a pixel whose 2-sample
+        // probe traced >= 16 segments goes to a drain before its first sample -- the
+        // longest chains then start draining at once instead of after ~6 ms in a
+        // cursor lane (N=8 rank 53.2-53.6 -> 49.6-51.4 ms, N=4 with the priority waves
+        // above 61.4-61.7 ms; N=1 and N=2 lose 25-40 % with them: knobs_small_shard_
+        // parking.log)
+        P.rate_k = 16, P.rate_x = small_fill ? 12u : 16u;
+        P.prepark = small_fill && P.order_map ? kSmallShardPrepark : 0u;
         // endgame parking: one pixel per drain group once the cursor is dry, in shards
         // of fewer than 2 pixels per lane of the launch (strong scaling at N >= 4: the
         // last chains set the time; N=8 rank 86 -> 65 ms). Full images lose by it (the

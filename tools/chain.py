@@ -10,7 +10,8 @@ import torch
 
 import raytracing_in_a_weekend_rust_amd as rtw
 
-W, H, S, ROW = 1200, 675, 23, 455
+W, H, S = 1200, 675, 23
+ROW = int(os.environ.get("CHAIN_ROW", "455"))
 os.environ["RTW_DIAG"] = "1"
 seed = rtw.DEFAULT_SEED
 cam, sph, n, mt, nm = rtw.builtin_scene("complex", seed, H, W, 50)

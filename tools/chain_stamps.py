@@ -11,7 +11,8 @@ os.environ.setdefault("RTW_BUDGET_X", "100000")  # RTW_BUDGET_X=10: heavy pixels
 import raytracing_in_a_weekend_rust_amd as rtw  # noqa: E402
 from raytracing_in_a_weekend_rust_amd import _capi as capi  # noqa: E402
 
-W, H, S, ROW = 1200, 675, int(os.environ.get("CHAIN_S", "23")), 455
+W, H, S = 1200, 675, int(os.environ.get("CHAIN_S", "23"))
+ROW = int(os.environ.get("CHAIN_ROW", "455"))
 cam, sph, n, mt, nm = rtw.builtin_scene("complex", rtw.DEFAULT_SEED, H, W, 50)
 for _ in range(2):
     fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, S, rtw.DEFAULT_SEED, shard=(ROW, H, 1))
