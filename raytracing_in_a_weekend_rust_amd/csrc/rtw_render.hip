@@ -1222,12 +1222,18 @@ __device__ __forceinline__ void dpp_min_step(double &bt, int &best) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(bt), kCtrl, 0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(bt), kCtrl, 0xf, 0xf, false);
     const double ot = __hiloint2double(hi, lo);
-    if (ob >= 0 && rtw_accel::better(ot, static_cast<uint32_t>(ob), bt, best)) bt = ot, best = ob;
+    // selects, not a branch: every lane of the wave runs the step (a branch cost the
+    // exec-mask bookkeeping of a divergent if on the drain's serial chain)
+    const bool take = (ob >= 0) & ((best < 0) | (ot < bt) | ((ot == bt) & (ob < best)));  // rtw_accel::better
+    bt = take ? ot : bt;
+    best = take ? ob : best;
 }
 __device__ __forceinline__ void shfl_min_step(double &bt, int &best, int off) {
     const int ob = __shfl_xor(best, off);
     const double ot = __shfl_xor(bt, off);
-    if (ob >= 0 && rtw_accel::better(ot, static_cast<uint32_t>(ob), bt, best)) bt = ot, best = ob;
+    const bool take = (ob >= 0) & ((best < 0) | (ot < bt) | ((ot == bt) & (ob < best)));  // rtw_accel::better
+    bt = take ? ot : bt;
+    best = take ? ob : best;
 }
 template <uint32_t kG>
 __device__ __forceinline__ void group_min(double &bt, int &best) {
@@ -2911,13 +2917,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // waves that signal the end of their cursor loop: priority waves too when they join
         P.n_cursor_waves = P.join_at != 0xffffffffu ? grid_p * wpb : grid_p * (wpb - heavy);
         // Park rules. Full images: after 16 samples above 16 segments per sample. Small
-        // shards (spare or half the waves drain): above 12, and a pixel whose 2-sample
+        // shards (spare or half the waves drain): above 10, and a pixel whose 2-sample
         // probe traced >= 16 segments goes to a drain before its first sample -- the
         // longest chains then start draining at once instead of after ~6 ms in a
-        // cursor lane (N=8 rank 53.2-53.6 -> 49.6-51.4 ms, N=4 with the priority waves
-        // above 61.4-61.7 ms; N=1 and N=2 lose 25-40 % with them: knobs_small_shard_
-        // parking.log)
-        P.rate_k = 16, P.rate_x = small_fill ? 12u : 16u;
+        // cursor lane (N=8 rank 53.2-53.6 -> 48.3-50.8 ms, N=4 with the priority waves
+        // above 61.3-61.8 ms; N=1 and N=2 lose 25-40 % with them: knobs_small_shard_
+        // parking.log, knobs_tail_rate.log)
+        P.rate_k = 16, P.rate_x = small_fill ? 10u : 16u;
         P.prepark = small_fill && P.order_map ? kSmallShardPrepark : 0u;
         // endgame parking: one pixel per drain group once the cursor is dry, in shards
         // of fewer than 2 pixels per lane of the launch (strong scaling at N >= 4: the
