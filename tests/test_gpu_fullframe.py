@@ -4,8 +4,10 @@ tests/golden/make_fullframe.py rendered BASELINE configs[2] (1200x675, s=10) and
 the headline workload (1200x675, s=23) with the C oracle in this container and
 committed the SHA-256 of each f64 framebuffer and PPM, the segment count and a
 short hash per row. Here the HIP path renders the same frames -- through the
-one-shot ABI and through the multi-device ABI with two sessions (the row-cyclic
-config-4 split) -- and must reproduce all of it: every one of the 675 rows."""
+one-shot ABI and through the multi-device ABI with 2, 4 and 8 sessions on the one
+GPU (the row-cyclic config-4 splits; their shard sizes take the small-shard
+scheduling: half the waves draining at 4, probe-hot pixels parked before their first
+sample at 4 and 8) -- and must reproduce all of it: every one of the 675 rows."""
 import hashlib
 import os
 
@@ -35,7 +37,7 @@ def test_fixtures_present():
     assert {"fullframe_complex_1200x675_s10_d50", "fullframe_complex_1200x675_s23_d50"} <= set(FRAMES)
 
 
-@pytest.mark.parametrize("via", ["one_shot", "multi2"])
+@pytest.mark.parametrize("via", ["one_shot", "multi2", "multi4", "multi8"])
 @pytest.mark.parametrize("frame", FRAMES)
 def test_full_frame_bit_exact(frame, via):
     fix = load(frame)
@@ -45,5 +47,6 @@ def test_full_frame_bit_exact(frame, via):
     if via == "one_shot":
         fb, st = rtw.render_flat(cam.raw, sph, n, mt, nm, fix["samples_sqrt"], seed)
     else:
-        fb, st = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, fix["samples_sqrt"], seed, devices=[0, 0])
+        fb, st = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, fix["samples_sqrt"], seed,
+                                       devices=[0] * int(via[len("multi"):]))
     check_frame(fb, st, fix)
