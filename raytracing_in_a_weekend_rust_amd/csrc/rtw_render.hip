@@ -1237,6 +1237,24 @@ __device__ __forceinline__ void shfl_min_step(double &bt, int &best, int off) {
 }
 template <uint32_t kG>
 __device__ __forceinline__ void group_min(double &bt, int &best) {
+    if constexpr (kG == 64) {
+#ifndef RTW_GROUP_MIN_FULL  // A/B: always the full reduction
+        // most segments leave at most one lane of the group with a hit (the scan spreads
+        // a segment's 1-2 candidates over the lanes, and a miss leaves none): that lane's
+        // record is the minimum -- broadcast it (wave-uniform branch) instead of six
+        // reduction steps on the drain's serial chain
+        const uint64_t hm = __ballot(best >= 0);
+        if ((hm & (hm - 1ull)) == 0ull) {
+            if (hm) {
+                const int src = __builtin_ctzll(hm);
+                best = __builtin_amdgcn_readlane(best, src);
+                bt = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(bt), src),
+                                      __builtin_amdgcn_readlane(__double2loint(bt), src));
+            }
+            return;
+        }
+#endif
+    }
     dpp_min_step<0xB1>(bt, best);   // quad_perm [1,0,3,2]
     dpp_min_step<0x4E>(bt, best);   // quad_perm [2,3,0,1]
     dpp_min_step<0x141>(bt, best);  // row_half_mirror
@@ -1301,6 +1319,14 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
         const bool cand = sub < n ? (disc >= 0. && t >= 0.01) : sub == n;
         bt = sub == n ? tf : t;
         best = cand ? static_cast<int>(i) : -1;
+        if constexpr (kG == 64) {  // S alone (no list entry hit): its far root, broadcast
+            if (__ballot(cand) == (1ull << n)) {
+                best = prev;
+                bt = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(bt), __builtin_amdgcn_readfirstlane(static_cast<int>(n))),
+                                      __builtin_amdgcn_readlane(__double2loint(bt), __builtin_amdgcn_readfirstlane(static_cast<int>(n))));
+                return true;
+            }
+        }
         dpp_min_step<0xB1>(bt, best);   // quad_perm [1,0,3,2]
         dpp_min_step<0x4E>(bt, best);   // quad_perm [2,3,0,1]
         dpp_min_step<0x141>(bt, best);  // row_half_mirror
