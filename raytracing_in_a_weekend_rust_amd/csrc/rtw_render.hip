@@ -75,6 +75,7 @@ constexpr double kBudgetX = 14.0;
 constexpr double kTailSegsPerSample = 768. / 529.;
 constexpr uint32_t kHeavyPerBlock = 2;  // priority waves per persistent workgroup (parked pixels)
 constexpr uint32_t kHeavyPerBlockFull = 6;  // ... in a shard of about one pixel per lane
+constexpr uint32_t kHeavyPerBlockFullShort = 4;  // ... of fewer than 400 samples per pixel
 constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 samples) that park a
                                             // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
@@ -2923,7 +2924,10 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // knobs_heavy_rate_endgame.log)
         const double fill = static_cast<double>(npix) / (static_cast<double>(grid_p) * pblock);
         const bool small_fill = fill < 1.5;  // strong scaling at N >= 4 of the bench image
-        uint32_t heavy = fill >= 0.75 && small_fill ? kHeavyPerBlockFull : kHeavyPerBlock;
+        // (fewer samples per pixel, shorter chains, fewer drains wanted: 4 at 100 spp,
+        // rank 23.0 -> 17.9 ms at s=10 with the rate rule's earlier start below)
+        uint32_t heavy = fill >= 0.75 && small_fill ? (P.n_off >= 400u ? kHeavyPerBlockFull : kHeavyPerBlockFullShort)
+                                                    : kHeavyPerBlock;
         if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
@@ -2949,7 +2953,10 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // cursor lane (N=8 rank 53.2-53.6 -> 48.3-50.8 ms, N=4 with the priority waves
         // above 61.3-61.8 ms; N=1 and N=2 lose 25-40 % with them: knobs_small_shard_
         // parking.log, knobs_tail_rate.log)
-        P.rate_k = 16, P.rate_x = small_fill ? 10u : 16u;
+        // In small shards the rate rule starts after ~3 % of the samples (16 of 529, 4 of
+        // 100: N=8 rank at s=10 16.3 -> 12.0-12.2 ms, knobs_s10_rate_heavy.log)
+        P.rate_k = small_fill ? std::max(4u, static_cast<uint32_t>(std::lround(16. * P.n_off / 529.))) : 16u;
+        P.rate_x = small_fill ? 10u : 16u;
         P.prepark = small_fill && P.order_map ? kSmallShardPrepark : 0u;
         // endgame parking: one pixel per drain group once the cursor is dry, in shards
         // of fewer than 2 pixels per lane of the launch (strong scaling at N >= 4: the
