@@ -990,25 +990,15 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
                     // waves run at priority 0 otherwise (hot waves: RTW_HOT_PRIO, off).
                     if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(kWalkPrio);
                     walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
-#ifndef RTW_PRIO_EXACT
                     if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
-#endif
                 }
                 STAMP(2);  // 2: BVH walk
-                if (!walked) {
-#ifdef RTW_PRIO_EXACT
-                    if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
-#endif
-                    return false;
-                }
+                if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
                     ++tl.ntest;
                     exact_test(sph, ws.cand_at(j), ox, oy, oz, dx, dy, dz,
                                a, best, bt);
                 }
-#ifdef RTW_PRIO_EXACT  // A/B: the candidates' exact tests raised too
-                if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
-#endif
                 return true;
             };
             bool walked;
@@ -2035,13 +2025,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 if (best >= 0 && KP(att_finite)) {  // black leaf: +-0, no fold (see trace_samples)
                     p.stk.clear();
                 } else {
-#ifdef RTW_PRIO_FOLD  // A/B: the fold's load chain raised
-                    __builtin_amdgcn_s_setprio(1);
-#endif
                     fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
-#ifdef RTW_PRIO_FOLD
-                    __builtin_amdgcn_s_setprio(0);
-#endif
                     acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 }
                 done = ++ps.k >= P.n_off;
@@ -2103,9 +2087,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             U128 own = ps.rng;  // the lane's own state (phase 3 runs on a copy)
             bool did3 = phase == 3u;
             bool any_real = __any(phase <= 2u);  // a lane leaves once finished; all, once no
-#ifdef RTW_PRIO_DRAWS  // A/B: the rejection loop's integer chains raised
-            __builtin_amdgcn_s_setprio(1);
-#endif
             while (any_real && phase <= 3u) {    // lane has a draw it needs
                 STAMP_CNT(0, 1u);
                 U128 st = ps.rng;
@@ -2139,9 +2120,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 phase = next;
                 any_real = __any(phase <= 2u);
             }
-#ifdef RTW_PRIO_DRAWS
-            __builtin_amdgcn_s_setprio(0);
-#endif
             spec = did3;
             if (did3) {  // keep the resume point (the accepting try's start, or the next try's),
                          // back to the lane's own state
