@@ -157,7 +157,9 @@ struct KParams {
     uint32_t probe_sub;         // cost probe on every probe_sub-th pixel of every probe_sub-th row
     uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
                                 // pixel; the leftover launch finishes them all
-    uint32_t drain_prio;        // draining waves raise their issue priority (RTW_DRAIN_PRIO, default 1)
+    uint32_t drain_prio;        // draining waves' issue priority after the cursor phase (RTW_DRAIN_PRIO,
+                                // default 3; 0: unchanged)
+    uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
     uint32_t plist_thlog, plist_tx;  // camera-ray lists: log2 of the tile height (shard rows),
                                      // tiles per row (tiles are 8 pixels wide)
     uint32_t hot_tickets;       // waves holding one of the first hot_tickets pixels of the cost order
@@ -1181,6 +1183,15 @@ __device__ __forceinline__ void diag_event(const KParams &P, uint64_t npix, uint
     if (d && KP(diag_ev))
         atomicCAS(d + 2 * npix + 4 + 3 * pix + k, 0u, static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()) | 1u);
 }
+// s_setprio takes an immediate: a run-time level (0-3) by a wave-uniform switch
+__device__ __forceinline__ void set_prio(uint32_t level) {
+    switch (level) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
 __device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
     return __hip_atomic_load((gu32 *)(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1773,7 +1784,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     // may never be published), and then count as cursor waves
     bool cursor_wave = !heavy_wave;
     if (heavy_wave) {
-        __builtin_amdgcn_s_setprio(3);
+        set_prio(KP(heavy_prio));
         const uint32_t sub = threadIdx.x & (kCoopG - 1u);
         const int gl = static_cast<int>(lane & ~(kCoopG - 1u));
         uint32_t cseg = 0;
@@ -2198,7 +2209,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     // a wave that drains runs one pixel's serial chain for the whole wave: raised
     // issue priority (as the priority waves), so the chains that set the launch's end
     // are not held back by the cursor waves still sharing the SIMD (RTW_DRAIN_PRIO=0: off)
-    if (KP(drain_prio)) __builtin_amdgcn_s_setprio(3);
+    if (KP(drain_prio)) set_prio(KP(drain_prio));
     for (bool drain = !KP(drain_off); drain;) {
         uint32_t t = 0, state = 0;  // state 1: ticket t is published, 2: stop
         if (sub == 0) {
@@ -2984,11 +2995,16 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
-        P.drain_prio = 1;
+        // priority waves drain at raised issue priority only in small shards, where the
+        // drained chains set the end; in a full image they have the time and their
+        // issue-bound segments would take slots from the cursor waves (N=1 123.6 ->
+        // 122.2 ms with 0; N=4 rank 60.0 -> 63.1 ms with 0: ab_heavy_prio.log)
+        P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
+        if (const char *e = std::getenv("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (const char *e = std::getenv("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
         if (const char *e = std::getenv("RTW_HOT_PRIO"))  // percent of the shard's pixels
             P.hot_tickets = P.order_map ? static_cast<uint32_t>(std::atof(e) / 100. * static_cast<double>(npix)) : 0u;
-        if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = std::atoi(e) != 0 ? 1u : 0u;
+        if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};

@@ -223,7 +223,7 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_ENDGAME", "100000000" if endgame else "0")
     monkeypatch.setenv("RTW_PROBE_SUB", coop[5:] if coop.startswith("probe") else "1")
     monkeypatch.setenv("RTW_PREPARK", "4" if coop == "prepark" else "0")
-    monkeypatch.setenv("RTW_DRAIN_PRIO", "0" if coop == "drainprio0" else "1")
+    monkeypatch.setenv("RTW_DRAIN_PRIO", "0" if coop == "drainprio0" else "3")
     monkeypatch.setenv("RTW_PLIST", "1" if coop == "plist1" else "0")
     if coop == "endgame_coopg16":
         monkeypatch.setenv("RTW_COOPG", "16")
