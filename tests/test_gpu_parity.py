@@ -101,6 +101,9 @@ def test_config2_three_lambertian_full_image():
     ("simple", 54, 96, 25, 2),      # the reference's simple(): dielectric + metal fuzz 0
     ("threads", 40, 40, 50, 2),
     ("three_lambertian", 23, 41, 8, 4),
+    ("complex", 1, 1, 50, 3),       # one pixel: one lane of one wave, every other idle
+    ("complex", 1, 37, 50, 2),      # one row
+    ("complex", 23, 1, 50, 2),      # one column
 ])
 def test_scenes_bit_exact(scene, h, w, d, s):
     cam, sph, n, mt, nm = rtw.builtin_scene(scene, SEED + 1, h, w, d)
@@ -497,6 +500,16 @@ def test_multi_device_abi_matches_single_device(devices):
     fb, mst = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 3, SEED, devices=devices)
     assert np.array_equal(fb, ref)
     assert mst.segments == st.segments and mst.pixels == 61 * 96 and mst.samples == st.samples
+
+
+def test_multi_device_more_entries_than_rows():
+    """Device entries beyond the image's rows get no rows (rows r = i mod n with
+    n = min(entries, H)); the image is still the single-device one."""
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 3, 17, 50)
+    ref, st = gpu(cam, sph, n, mt, nm, 2, SEED)
+    fb, mst = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 2, SEED, devices=[0] * 5)
+    assert np.array_equal(fb, ref)
+    assert mst.segments == st.segments and mst.pixels == 3 * 17
 
 
 def test_shutdown_frees_and_recreates_sessions():
