@@ -443,8 +443,6 @@ struct Path {
     double ox, oy, oz, dx, dy, dz;
     uint32_t depth;
     int prev;  // sphere of the last hit (-1: camera ray): the inside-cut hint
-    uint32_t prev_info;  // drain groups (kTrap): prev's inside-cut info word, read with its
-                         // shading record (one LDS round trip fewer on the serial chain)
     PathStack stk;
 };
 
@@ -676,9 +674,6 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     p.ox = px, p.oy = py, p.oz = pz;
     p.dx = ndx, p.dy = ndy, p.dz = ndz;
     p.prev = best;
-#ifdef RTW_INFO_CARRY
-    if constexpr (kTrap) p.prev_info = M.nbr;
-#endif
     ++p.depth;
     return p.depth >= P.max_depth;  // ray_color(depth >= max) -> black
 }
@@ -788,9 +783,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         ++seg;
         const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
         double bt = 0.;
-        int best;
-        if constexpr (kTrap) best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, p.prev_info);
-        else best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
+        const int best = hit(p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt);
         STAMP(1);
         double lr, lg, lb;
         TrapHint th;
@@ -1304,18 +1297,12 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
 // chain -- then the group's (t, index) minimum. Same result as inside_hit.
 template <uint32_t kG>
 __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph, const ShadeRec *__restrict__ shd,
-                                                 const uint16_t *__restrict__ nbr, int prev, uint32_t prev_info, double ox,
+                                                 const uint16_t *__restrict__ nbr, int prev, double ox,
                                                  double oy, double oz, double dx, double dy, double dz, double a,
                                                  int &best, double &bt, Tally &tl, uint32_t sub) {
     static_assert(rtw_accel::kMaxNbr <= kG, "one list entry per lane");
     if (prev < 0) return false;
-#ifndef RTW_INFO_CARRY  // opt-in A/B: the info word carried from the shading record
     const uint32_t info = shd[prev].nbr;
-    (void)prev_info;
-#else
-    const uint32_t info = prev_info;  // == shd[prev].nbr (Path::prev_info)
-    (void)shd;
-#endif
     if (info == rtw_accel::kNbrNone) return false;
     const uint32_t n = info & 0xffu;  // group-uniform, <= kMaxNbr < 16
 #ifndef RTW_INSIDE_SERIAL  // A/B: -DRTW_INSIDE_SERIAL tests S first, then the list
@@ -1437,12 +1424,12 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u) << fsh];
     }
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
-                   double &bt, uint32_t prev_info) -> int {
+                   double &bt) -> int {
         int best = -1;
         bt = 0.;
         // inside cut: every lane of the group holds the same path, so the branch
         // is group-uniform and the lanes run the (short) list redundantly
-        if (inside_hit_group<kG>(sph, sv.shd, sv.nbr, prev, prev_info, ox, oy, oz, dx, dy, dz, a, best, bt, tl, sub))
+        if (inside_hit_group<kG>(sph, sv.shd, sv.nbr, prev, ox, oy, oz, dx, dy, dz, a, best, bt, tl, sub))
             return best;
         const Seg32 g(ox, oy, oz, dx, dy, dz, a, true);
         STAMP(0);  // coop: loop back + segment setup (Seg32)
