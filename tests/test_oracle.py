@@ -159,6 +159,23 @@ def test_c_and_python_oracles_agree_on_rows_of_final_scene():
     assert seg == pseg
 
 
+@pytest.mark.parametrize("h,w,s", [(1, 1, 3), (1, 13, 2), (9, 1, 2)])
+def test_c_and_python_oracles_agree_on_degenerate_images(h, w, s):
+    """One pixel, one row, one column: the camera's pixel deltas and the RNG
+    chain's pixel order (camera.rs:223-260) at the shapes the GPU parity tests
+    also render."""
+    seed = 11
+    pc, objs = py.scene_builtin("complex", seed, h, w, 50)
+    cam = c_camera(pc)
+    sph, mat = c_scene(objs)
+    fb, seg = orc.render(cam, sph, len(objs), mat, len(objs), s, seed)
+    img, pseg = py.render(pc, objs, s, seed, rows=list(range(h)))
+    for y in range(h):
+        for x in range(w):
+            assert tuple(fb[y, x]) == img[(x, y)]
+    assert seg == pseg
+
+
 def test_schedulers_agree():
     pc, objs = py.scene_builtin("complex", 99, 27, 48, 50)
     cam = c_camera(pc)
