@@ -38,6 +38,11 @@ $(OUT)/rtw_fast.o: $(SRC)/rtw_fast.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h incl
 	@mkdir -p $(OUT)
 	$(HIPCC) $(filter-out -ffp-contract=off,$(HIPFLAGS)) -ffp-contract=fast -c $< -o $@
 
+# multi-GPU groups (RCCL gather, opened with dlopen at first use)
+$(OUT)/rtw_group.o: $(SRC)/rtw_group.hip include/rtw_capi.h $(SRC)/host/rtw_internal.h
+	@mkdir -p $(OUT)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(OUT)/rtw_accel_build.o: $(SRC)/host/rtw_accel_build.cpp $(SRC)/rtw_accel.h
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -I$(SRC) -c $< -o $@
@@ -63,8 +68,8 @@ $(OUT)/rtw_host.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_h
 	@mkdir -p $(OUT)
 	$(CXX) $(CXXFLAGS) -I$(OUT) -c $< -o $@
 
-$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
-	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread
+$(OUT)/librtw.so: $(OUT)/rtw_render.o $(OUT)/rtw_fast.o $(OUT)/rtw_group.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
+	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw.so -lpthread -ldl
 
 $(OUT)/rtw_cli: $(SRC)/host/rtw_cli.cpp $(OUT)/librtw.so
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN' -lpthread
@@ -76,7 +81,7 @@ oracle:
 stamps: $(OUT)/librtw_stamps.so
 $(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
 	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
-$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
+$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_group.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
 asm: $(SRC)/rtw_render.hip

@@ -11,11 +11,17 @@ equivalent, camera.rs:223-352) with the scene already resident in HBM.
 (config 3: --samples-sqrt 10; a config-5 rank: --size 4096x2304 --samples-sqrt 45
 under torchrun --nproc-per-node 8).
 
-N>1 (one rank per GPU, BASELINE configs[3]'s scaling curve): by default the ONE
-frame is sharded row-cyclically over the ranks (row r -> rank r % N) and gathered
-over RCCL (all_gather of the padded row tiles + un-permute) inside the timed step;
-`--scaling weak` renders one whole frame per rank instead (render seed SEED + rank,
-no collective).
+N>1, BASELINE configs[3]'s scaling curve, two launch shapes, both row-cyclic
+(row r -> GPU r % N) with the gather inside the timed step:
+  * `python bench.py --gpus N` (one process): an rtw_group of N device entries
+    (include/rtw_capi.h) -- one session and stream per GPU, the row tiles gathered
+    on GPU 0 by one ncclGather over xGMI and un-permuted there. On a box with fewer
+    than N GPUs the entries repeat the visible devices round-robin (the line then
+    says "devices repeated; not a scaling point").
+  * `torchrun --nproc-per-node N bench.py --gpus N` (one rank per GPU): each rank
+    renders its rows, then an RCCL all_gather of the padded row tiles + un-permute
+    (torch.distributed); `--scaling weak` renders one whole frame per rank instead
+    (render seed SEED + rank, no collective).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size WxH] [--samples-sqrt S]
                     [--depth D] [--scaling strong|weak] [--mode parity|fast]
@@ -290,18 +296,32 @@ def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
 
 
 def parity_check(a, image, segments):
-    """The timed frame against the committed full-frame oracle fixture
-    (tests/golden/make_fullframe.py), outside the timed region."""
-    path = os.path.join(HERE, "tests", "golden", f"fullframe_{workload_name(a)}.json")
-    if a.mode != "parity" or not os.path.exists(path):
+    """The timed frame against the committed oracle fixture, outside the timed region:
+    the full-frame fixture (tests/golden/make_fullframe.py) when the workload has one,
+    else its row sample (config 5: the sampled rows' SHA-256)."""
+    if a.mode != "parity":
         return None
-    with open(path) as f:
-        fix = json.load(f)
-    fb = image.contiguous().cpu().numpy().astype("<f8", copy=False)
-    ok = hashlib.sha256(fb.tobytes()).hexdigest() == fix["fb_sha256"]
-    return {"fixture": os.path.relpath(path, HERE), "fb_sha256_ok": ok,
-            "segments_ok": segments == fix["segments"], "segments": segments,
-            "note": "last timed frame (gathered on rank 0 at N>1) vs the C oracle's full frame"}
+    full = os.path.join(HERE, "tests", "golden", f"fullframe_{workload_name(a)}.json")
+    rows = os.path.join(HERE, "tests", "golden", f"rowsample_{workload_name(a)}.json")
+    if os.path.exists(full):
+        with open(full) as f:
+            fix = json.load(f)
+        fb = image.contiguous().cpu().numpy().astype("<f8", copy=False)
+        ok = hashlib.sha256(fb.tobytes()).hexdigest() == fix["fb_sha256"]
+        return {"fixture": os.path.relpath(full, HERE), "fb_sha256_ok": ok,
+                "segments_ok": segments == fix["segments"], "segments": segments,
+                "note": "last timed frame (gathered on rank 0 at N>1) vs the C oracle's full frame"}
+    if os.path.exists(rows):
+        with open(rows) as f:
+            fix = json.load(f)
+        fb = image.contiguous().cpu().numpy().astype("<f8", copy=False)
+        bad = [y for y, h in zip(fix["rows"], fix["row_sha256"])
+               if hashlib.sha256(fb[y].tobytes()).hexdigest() != h]
+        return {"fixture": os.path.relpath(rows, HERE), "rows_checked": len(fix["rows"]),
+                "rows_sha256_ok": not bad, "rows_differing": bad[:16], "segments": segments,
+                "note": "last timed frame's sampled rows vs the C oracle's row sample "
+                        "(the full frame is ~6 h of oracle time)"}
+    return None
 
 
 # ---------------------------------------------------------------- roofline --
@@ -363,6 +383,91 @@ def roofline(a, st, kms, main_ms, pm, pm_source, n_cu, grid):
     return r
 
 
+def base_line(a, value, elapsed, n_gpus, frames, ns):
+    fast = a.mode == "fast"
+    W, H, s = a.width, a.height, a.samples_sqrt
+    return {
+        "metric": "Msamples/sec (pixels×spp) on final-scene 1200×675 spp=500 d=50; CPU-ref speedup",
+        "value": round(value, 3),
+        "unit": "Msamples/s",
+        "n_gpus": n_gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak" if a.scaling == "weak" else "strong",
+        "vs_baseline": None,
+        "dtype": "f32" if fast else "f64",
+        "data": "synthetic (the reference's own procedural final scene, fixed seed)",
+        "config": {"workload": workload_name(a), "width": W, "height": H,
+                   "samples_sqrt": s, "spp": s * s if s else 1, "max_depth": a.depth,
+                   "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED, "frames": frames,
+                   "mode": ("fast_f32 (statistical parity; xoroshiro64** per (pixel, sample))"
+                            if fast else "parity_f64 (bit-exact)")},
+    }
+
+
+def group_main(a, torch, rtw, shard):
+    """`python bench.py --gpus N` as a plain command: one process drives N device
+    entries through an rtw_group (one session + stream per GPU, rows r -> entry
+    r % N, ncclGather of the row tiles to GPU 0 + un-permute there, inside every
+    timed step; rtw_group_render is blocking). Reference: camera.rs:253 -- the
+    reference's pool takes every core of the machine from one call."""
+    if a.scaling == "weak" or a.sim:
+        raise SystemExit("--scaling weak / --shard-of run under torchrun (one rank per GPU)")
+    visible = rtw.device_count()
+    devs, repeated = shard.group_devices(a.gpus, visible)
+    W, H, s = a.width, a.height, a.samples_sqrt
+    cam, sph, ns, mt, nm = rtw.builtin_scene("complex", SEED, H, W, a.depth)
+    fast = a.mode == "fast"
+    g = rtw.Group(devs)
+    g.set_scene(sph, ns, mt, nm)
+    image = torch.empty((H, W, 3), dtype=torch.float32 if fast else torch.float64,
+                        device=torch.device("cuda", devs[0]))
+    render = g.render_fast if fast else g.render
+
+    def sync_all():
+        for d in sorted(set(devs)):
+            torch.cuda.synchronize(d)
+
+    for _ in range(a.warmup):
+        render(cam.raw, s, SEED, image.data_ptr())
+    sync_all()
+    t0 = time.perf_counter()
+    walls, roots = [], []
+    for _ in range(a.steps):
+        render(cam.raw, s, SEED, image.data_ptr())
+        _, _, info = g.stats()
+        walls.append(info["wall_ms"])
+        roots.append(info["root_gather_ms"])
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    total, per, info = g.stats()
+    value = W * H * (s * s if s else 1) * a.steps / elapsed / 1e6
+    out = base_line(a, value, elapsed, a.gpus, 1, ns)
+    out["config"]["parallelism"] = (
+        f"one process, rtw_group of {a.gpus} entries on devices {devs}, row-cyclic, gather "
+        f"{info['gather']} to device {devs[0]} + un-permute there"
+        + ("; devices repeated; not a scaling point" if repeated else ""))
+    out["group"] = {"devices": devs, "visible_devices": visible, "repeated": repeated,
+                    "gather": info["gather"],
+                    "entry_kernel_ms": [round(p.kernel_ms, 3) for p in per],
+                    "entry_main_kernel_ms": [round(p.main_kernel_ms, 3) for p in per],
+                    "entry_pixels": [p.pixels for p in per],
+                    "last_wall_ms": round(info["wall_ms"], 3),
+                    "last_render_ms_max": round(info["render_ms_max"], 3),
+                    "mean_root_gather_ms": round(sum(roots) / len(roots), 3),
+                    "mean_wall_ms": round(sum(walls) / len(walls), 3),
+                    "note": "root_gather_ms: GPU 0's stream from its own tile rendered to the image "
+                            "complete (waiting for the slowest entry + gather + un-permute)"}
+    n_cu = torch.cuda.get_device_properties(devs[0]).multi_processor_count * len(set(devs))
+    out["roofline"] = roofline(a, total, info["render_ms_max"], max(p.main_kernel_ms for p in per),
+                               None, "not collected (N>1)", n_cu, total.grid_blocks)
+    out["parity"] = parity_check(a, image, total.segments)
+    print(json.dumps(out), flush=True)
+    g.close()
+
+
 def main():
     a = parse()
     if a.pmc_child:
@@ -377,8 +482,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world == 1 and a.gpus > 1:
-        raise SystemExit("--gpus N>1 needs torchrun --nproc-per-node N (one rank per GPU)")
+    if world == 1 and a.gpus > 1:
+        return group_main(a, torch, rtw, shard)
+    if world != a.gpus and a.gpus > 1:
+        raise SystemExit(f"--gpus {a.gpus} under a launcher of WORLD_SIZE {world}: one rank per GPU, "
+                         "or drop the launcher (one process drives every GPU)")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -465,27 +573,11 @@ def main():
             if pm is None and a.mode == "parity" and workload_name(a) == "complex_1200x675_s23_d50":
                 pm, fb_why = pmc_fallback(MAIN_KERNEL[a.mode], rtw.build_id())
                 pm_source = (pm_source + "; " if a.pmc else "") + fb_why
-        out = {
-            "metric": "Msamples/sec (pixels×spp) on final-scene 1200×675 spp=500 d=50; CPU-ref speedup",
-            "value": round(value, 3),
-            "unit": "Msamples/s",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak" if weak else "strong",
-            "vs_baseline": None,
-            "dtype": "f32" if fast else "f64",
-            "data": "synthetic (the reference's own procedural final scene, fixed seed)",
-            "config": {"workload": workload_name(a), "width": W, "height": H,
-                       "samples_sqrt": s, "spp": n_off, "max_depth": DEPTH,
-                       "n_spheres": ns, "scene_seed": SEED, "render_seed": SEED, "frames": frames,
-                       "parallelism": (f"rank {a.sim[1]} of a row-cyclic x{a.sim[0]} split, alone on one "
-                                       "GPU (value = this rank's samples / its time; the other ranks "
-                                       "not run)" if a.sim else plan.describe()),
-                       "mode": ("fast_f32 (statistical parity; xoroshiro64** per (pixel, sample))"
-                                if fast else "parity_f64 (bit-exact)")},
+        out = base_line(a, value, elapsed, world, frames, ns)
+        out["config"]["parallelism"] = (f"rank {a.sim[1]} of a row-cyclic x{a.sim[0]} split, alone on one "
+                                        "GPU (value = this rank's samples / its time; the other ranks "
+                                        "not run)" if a.sim else plan.describe())
+        out.update({
             "roofline": roofline(a, st, kms, st.main_kernel_ms or kms, pm, pm_source, n_cu, st.grid_blocks),
             "parity": parity,
             "build_id": rtw.build_id(),
@@ -500,7 +592,7 @@ def main():
                       "exact_wave_iters_per_wave_segment": round(st.exact_wave_iterations / max(1, st.wave_iterations), 3),
                       "inside_cut_fraction": round(st.inside_segments / max(1, st.segments), 4),
                       "trap_skipped_fraction": round(st.trap_segments / max(1, st.segments), 4)},
-        }
+        })
         if world == 1 and a.e2e:
             out["end_to_end"] = end_to_end(rtw, cam.raw, sph, ns, mt, nm, s, plan.render_seed, fast, kms, W * H)
         if world == 1 and a.cpu_baseline:

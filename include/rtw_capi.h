@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 6
+#define RTW_ABI_VERSION 7
 
 /* ---- error codes ---- */
 #define RTW_OK 0
@@ -197,6 +197,13 @@ int rtw_threaded_render_multi(const rtw_camera *cam, const rtw_sphere *spheres, 
                               rtw_u128 seed, const int *devices, uint32_t n_devices, double *out_rgb,
                               rtw_stats *stats);
 
+/* rtw_threaded_render_multi in f32 fast mode (ABI 7; see rtw_session_render_fast):
+ * same device list, row dealing and strided gather into out_rgb (host, H*W*3 f32). */
+int rtw_threaded_render_multi_fast(const rtw_camera *cam, const rtw_sphere *spheres,
+                                   uint32_t n_spheres, const rtw_material *mats, uint32_t n_mats,
+                                   uint32_t samples_sqrt, rtw_u128 seed, const int *devices,
+                                   uint32_t n_devices, float *out_rgb, rtw_stats *stats);
+
 /* rtw_threaded_render in f32 fast mode (see rtw_session_render_fast). */
 int rtw_threaded_render_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
                              const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
@@ -247,6 +254,47 @@ int rtw_session_stats(rtw_session *s, rtw_stats *out);
  * the pixel completed (0 = never ran); out[2 x pixels] = the clock at the persistent
  * launch's start. Returns RTW_E_CAPACITY if cap < 2 x pixels + 4. */
 int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap);
+
+/* ---- device-resident multi-GPU renders (ABI 7) ----
+ * A group is the node-level Camera::threaded_render (camera.rs:223-352; the
+ * reference's pool takes every core, camera.rs:253 -- a group takes every listed
+ * GPU) with the image left in HBM: one session per entry of `devices` (NULL or 0
+ * entries = every visible device; an index may repeat), image row r rendered by
+ * entry r % n, the row tiles gathered on the root device (entry 0) and
+ * un-permuted there into the caller's device buffer. The gather is one ncclGather
+ * over xGMI (RCCL communicators from ncclCommInitAll) when the entries are
+ * distinct GPUs, device-to-device copies otherwise (a repeated device, or
+ * RTW_GROUP_COPY_GATHER). Renders are blocking: on return the image is complete
+ * in out_rgb_device. Bit-identical to a one-device render. */
+typedef struct rtw_group rtw_group;
+#define RTW_GROUP_COPY_GATHER 1u /* flags: never RCCL, gather by device copies          */
+#define RTW_GROUP_RCCL_ALWAYS 2u /* flags: RCCL gather even for a one-entry group (tests) */
+enum { RTW_GATHER_NONE = 0, RTW_GATHER_COPY = 1, RTW_GATHER_RCCL = 2 };
+typedef struct rtw_group_info {
+    uint32_t n_entries;     /* entries that rendered rows in the last render (min(n, H)) */
+    uint32_t gather;        /* RTW_GATHER_* the last render used                        */
+    double wall_ms;         /* host wall time of the last rtw_group_render(_fast)       */
+    double render_ms_max;   /* slowest entry's render (HIP events on its own stream)     */
+    double root_gather_ms;  /* root stream, from its own tile rendered to the image
+                               complete: waiting for the other entries + gather +
+                               un-permute                                               */
+    uint32_t fast, _pad;    /* the last render was f32 fast mode                        */
+} rtw_group_info;
+int rtw_group_create(const int *devices, uint32_t n_devices, uint32_t flags, rtw_group **out);
+int rtw_group_destroy(rtw_group *g);
+int rtw_group_set_scene(rtw_group *g, const rtw_sphere *spheres, uint32_t n_spheres,
+                        const rtw_material *mats, uint32_t n_mats);
+/* out_rgb_device: H*W*3 f64 on the root device. */
+int rtw_group_render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                     double *out_rgb_device);
+/* f32 fast mode; out_rgb_device: H*W*3 f32 on the root device. */
+int rtw_group_render_fast(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt,
+                          rtw_u128 seed, float *out_rgb_device);
+/* Last render: total (counters summed, times the slowest entry's; nullable),
+ * per_entry[0..n_entries) (nullable; RTW_E_CAPACITY if cap < n_entries) and info
+ * (nullable). */
+int rtw_group_stats(rtw_group *g, rtw_stats *total, rtw_stats *per_entry, uint32_t cap,
+                    rtw_group_info *info);
 
 /* ---- device probes (tests) ---- */
 /* Device jump-ahead seeds (the kernel's own code path) for a pixel range. */

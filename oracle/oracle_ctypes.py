@@ -39,6 +39,10 @@ def lib():
         L.orc_render.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
                                  C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                                  C.c_uint32, C.c_uint32, C.c_int, P(C.c_double), P(C.c_uint64)]
+        L.orc_render_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                      C.c_uint32, C.c_uint64, C.c_uint64, P(C.c_uint32), C.c_uint32,
+                                      C.c_uint32, C.c_int, P(C.c_double), P(C.c_uint64),
+                                      P(C.c_uint64)]
         L.orc_format_ppm.restype = C.c_uint64
         L.orc_format_ppm.argtypes = [P(C.c_double), C.c_uint32, C.c_uint32, C.c_char_p, C.c_uint64]
         _lib = L
@@ -103,6 +107,25 @@ def render(cam, sph, n_sph, mats, n_mats, samples_sqrt, seed, rows=None, nthread
     if rc != 0:
         raise ValueError(f"orc_render failed: {rc}")
     return out, seg.value
+
+
+def render_rows(cam, sph, n_sph, mats, n_mats, samples_sqrt, seed, rows, nthreads=None,
+                scheduler=1):
+    """rows: ascending image-row indices. Returns (fb [len(rows), W, 3], segments,
+    per-row segments)."""
+    rows = np.ascontiguousarray(rows, dtype=np.uint32)
+    nthreads = nthreads or min(16, os.cpu_count() or 1)
+    out = np.zeros((len(rows), cam.img_width, 3), dtype=np.float64)
+    row_seg = np.zeros(len(rows), dtype=np.uint64)
+    seg = C.c_uint64()
+    rc = lib().orc_render_rows(C.byref(cam), C.byref(sph), n_sph, C.byref(mats), n_mats,
+                               samples_sqrt, *split(seed),
+                               rows.ctypes.data_as(C.POINTER(C.c_uint32)), len(rows), nthreads,
+                               scheduler, out.ctypes.data_as(C.POINTER(C.c_double)), C.byref(seg),
+                               row_seg.ctypes.data_as(C.POINTER(C.c_uint64)))
+    if rc != 0:
+        raise ValueError(f"orc_render_rows failed: {rc}")
+    return out, seg.value, row_seg
 
 
 def format_ppm(fb: np.ndarray) -> bytes:

@@ -395,9 +395,11 @@ typedef struct {
     uint32_t n_off;
     V3 *offsets;
     const u128 *children; /* per rendered pixel */
-    uint32_t row_begin, row_step, n_rows, W;
+    const uint32_t *rows; /* image row of each rendered row, ascending */
+    uint32_t n_rows, W;
     int faithful;
     double *out;
+    _Atomic uint64_t *row_segments; /* per rendered row (nullable) */
     _Atomic uint64_t next_job;
     _Atomic uint64_t segments;
 } Ctx;
@@ -477,7 +479,7 @@ static inline Ray get_ray(const orc_camera *cam, uint32_t i, uint32_t j, V3 offs
 /* camera.rs:354-374 */
 static void render_pixel(Ctx *c, uint64_t local_idx) {
     uint32_t lr = (uint32_t)(local_idx / c->W), x = (uint32_t)(local_idx % c->W);
-    uint32_t y = c->row_begin + lr * c->row_step;
+    uint32_t y = c->rows[lr];
     u128 rng = c->children[local_idx];
     uint64_t seg = 0;
     V3 acc = v3(0., 0., 0.);
@@ -491,6 +493,7 @@ static void render_pixel(Ctx *c, uint64_t local_idx) {
     o[1] = col.y;
     o[2] = col.z;
     atomic_fetch_add_explicit(&c->segments, seg, memory_order_relaxed);
+    if (c->row_segments) atomic_fetch_add_explicit(&c->row_segments[lr], seg, memory_order_relaxed);
 }
 
 static void *worker(void *arg) {
@@ -512,16 +515,16 @@ static void *worker(void *arg) {
     return NULL;
 }
 
-int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
-               const orc_material *mat, uint32_t n_mat, uint32_t samples_sqrt,
-               uint64_t seed_lo, uint64_t seed_hi, uint32_t row_begin, uint32_t row_step,
-               uint32_t n_rows, uint32_t nthreads, int scheduler, double *out,
-               uint64_t *segments) {
+static int render_rows(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
+                       const orc_material *mat, uint32_t n_mat, uint32_t samples_sqrt,
+                       uint64_t seed_lo, uint64_t seed_hi, const uint32_t *rows,
+                       uint32_t n_rows, uint32_t nthreads, int scheduler, double *out,
+                       uint64_t *segments, uint64_t *row_segments) {
     uint32_t W = cam->img_width, H = cam->img_height;
     if (W == 0 || H == 0) return -1; /* camera.rs:267 */
-    if (row_step == 0) row_step = 1;
     if (n_rows == 0) return 0;
-    if ((uint64_t)row_begin + (uint64_t)(n_rows - 1) * row_step >= H) return -2;
+    for (uint32_t k = 0; k < n_rows; ++k)
+        if (rows[k] >= H || (k && rows[k] <= rows[k - 1])) return -2;
     for (uint32_t i = 0; i < n_sph; ++i)
         if (sph[i].mat >= n_mat) return -3;
     for (uint32_t i = 0; i < n_mat; ++i)
@@ -532,9 +535,12 @@ int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
     memset(&c, 0, sizeof c);
     c.cam = cam;
     c.W = W;
-    c.row_begin = row_begin;
-    c.row_step = row_step;
+    c.rows = rows;
     c.n_rows = n_rows;
+    if (row_segments) {
+        memset(row_segments, 0, sizeof(uint64_t) * n_rows);
+        c.row_segments = (_Atomic uint64_t *)row_segments;
+    }
     c.faithful = scheduler == 0;
     c.out = out;
 
@@ -569,10 +575,10 @@ int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
      * whole image (camera.rs:255, 269-272), kept for the rendered rows only */
     u128 *children = (u128 *)malloc(sizeof(u128) * (uint64_t)n_rows * W);
     u128 parent = mk128(seed_lo, seed_hi);
-    uint32_t last_row = row_begin + (n_rows - 1) * row_step;
+    uint32_t last_row = rows[n_rows - 1];
     uint32_t next_lr = 0;
     for (uint32_t y = 0; y <= last_row; ++y) {
-        int keep = next_lr < n_rows && y == row_begin + next_lr * row_step;
+        int keep = next_lr < n_rows && y == rows[next_lr];
         for (uint32_t x = 0; x < W; ++x) {
             u128 ch = xs_copy_reset(&parent);
             if (keep) children[(uint64_t)next_lr * W + x] = ch;
@@ -593,6 +599,32 @@ int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
     free(mats);
     free(c.offsets);
     return 0;
+}
+
+int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
+               const orc_material *mat, uint32_t n_mat, uint32_t samples_sqrt,
+               uint64_t seed_lo, uint64_t seed_hi, uint32_t row_begin, uint32_t row_step,
+               uint32_t n_rows, uint32_t nthreads, int scheduler, double *out,
+               uint64_t *segments) {
+    if (cam->img_width == 0 || cam->img_height == 0) return -1; /* camera.rs:267 */
+    if (row_step == 0) row_step = 1;
+    if (n_rows == 0) return 0;
+    if ((uint64_t)row_begin + (uint64_t)(n_rows - 1) * row_step >= cam->img_height) return -2;
+    uint32_t *rows = (uint32_t *)malloc(sizeof(uint32_t) * n_rows);
+    for (uint32_t k = 0; k < n_rows; ++k) rows[k] = row_begin + k * row_step;
+    int rc = render_rows(cam, sph, n_sph, mat, n_mat, samples_sqrt, seed_lo, seed_hi, rows, n_rows,
+                         nthreads, scheduler, out, segments, NULL);
+    free(rows);
+    return rc;
+}
+
+int orc_render_rows(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
+                    const orc_material *mat, uint32_t n_mat, uint32_t samples_sqrt,
+                    uint64_t seed_lo, uint64_t seed_hi, const uint32_t *rows, uint32_t n_rows,
+                    uint32_t nthreads, int scheduler, double *out, uint64_t *segments,
+                    uint64_t *row_segments) {
+    return render_rows(cam, sph, n_sph, mat, n_mat, samples_sqrt, seed_lo, seed_hi, rows, n_rows,
+                       nthreads, scheduler, out, segments, row_segments);
 }
 
 /* ------------------------------------------------------------------ PPM --- */

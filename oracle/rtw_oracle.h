@@ -86,6 +86,15 @@ int orc_render(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
                uint32_t n_rows, uint32_t nthreads, int scheduler, double *out,
                uint64_t *segments);
 
+/* Render an explicit ascending list of image rows (same schedulers, same per-pixel
+ * children as a whole-image render). row_segments (nullable): traced segments per
+ * listed row. */
+int orc_render_rows(const orc_camera *cam, const orc_sphere *sph, uint32_t n_sph,
+                    const orc_material *mat, uint32_t n_mat, uint32_t samples_sqrt,
+                    uint64_t seed_lo, uint64_t seed_hi, const uint32_t *rows, uint32_t n_rows,
+                    uint32_t nthreads, int scheduler, double *out, uint64_t *segments,
+                    uint64_t *row_segments);
+
 /* Color::wire_full_file (color.rs:196-247). Writes into buf (cap bytes); returns
  * bytes needed (call with buf=NULL to size). */
 uint64_t orc_format_ppm(const double *rgb, uint32_t w, uint32_t h, char *buf, uint64_t cap);

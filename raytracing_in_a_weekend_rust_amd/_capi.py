@@ -79,6 +79,19 @@ class Stats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class GroupInfo(C.Structure):
+    _fields_ = [("n_entries", C.c_uint32), ("gather", C.c_uint32), ("wall_ms", C.c_double),
+                ("render_ms_max", C.c_double), ("root_gather_ms", C.c_double),
+                ("fast", C.c_uint32), ("_pad", C.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
+
+
+GATHER_NAMES = {0: "none", 1: "copy", 2: "rccl"}
+GROUP_COPY_GATHER = 1
+GROUP_RCCL_ALWAYS = 2
+
 RTW_OK = 0
 ERRORS = {-1: "RTW_E_ARG", -2: "RTW_E_EMPTY_IMAGE", -3: "RTW_E_FUZZ", -4: "RTW_E_MAT_INDEX",
           -5: "RTW_E_HIP", -6: "RTW_E_UNSUPPORTED", -7: "RTW_E_NO_DEVICE", -8: "RTW_E_CAPACITY"}
@@ -114,6 +127,16 @@ SIGNATURES = {
     "rtw_threaded_render_multi": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                             C.c_uint32, C.c_uint32, U128, _P(C.c_int), C.c_uint32,
                                             _P(C.c_double), _P(Stats)]),
+    "rtw_threaded_render_multi_fast": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
+                                                 C.c_uint32, C.c_uint32, U128, _P(C.c_int),
+                                                 C.c_uint32, _P(C.c_float), _P(Stats)]),
+    "rtw_group_create": (C.c_int, [_P(C.c_int), C.c_uint32, C.c_uint32, _P(C.c_void_p)]),
+    "rtw_group_destroy": (C.c_int, [C.c_void_p]),
+    "rtw_group_set_scene": (C.c_int, [C.c_void_p, _P(Sphere), C.c_uint32, _P(Material),
+                                      C.c_uint32]),
+    "rtw_group_render": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
+    "rtw_group_render_fast": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
+    "rtw_group_stats": (C.c_int, [C.c_void_p, _P(Stats), _P(Stats), C.c_uint32, _P(GroupInfo)]),
     "rtw_threaded_render_fast": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                            C.c_uint32, C.c_uint32, U128, _P(Shard),
                                            _P(C.c_float), _P(Stats)]),
@@ -155,6 +178,15 @@ def _load():
             f"librtw.so not built at {LIB_PATH}: run `make` (or __graft_entry__.build()). "
             "There is no fallback render path.")
     lib = C.CDLL(LIB_PATH)
+    # the ABI check comes before any other symbol is bound: a stale library that
+    # predates a symbol is reported as such, not as an AttributeError
+    if not hasattr(lib, "rtw_abi_version"):
+        raise ImportError(f"{LIB_PATH} predates rtw_abi_version (ABI < 6): rebuild with `make`")
+    lib.rtw_abi_version.restype = C.c_int
+    lib.rtw_abi_version.argtypes = []
+    if lib.rtw_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {lib.rtw_abi_version()}, this binding expects "
+                          f"{ABI_VERSION}: rebuild with `make`")
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
@@ -162,10 +194,8 @@ def _load():
     return lib
 
 
+ABI_VERSION = 7  # include/rtw_capi.h RTW_ABI_VERSION this binding's structs follow
 lib = _load()
-ABI_VERSION = 6  # include/rtw_capi.h RTW_ABI_VERSION this binding's structs follow
-if lib.rtw_abi_version() != ABI_VERSION:
-    raise ImportError(f"{LIB_PATH} has ABI {lib.rtw_abi_version()}, this binding expects {ABI_VERSION}")
 
 
 def check(rc: int) -> int:

@@ -150,10 +150,16 @@ class Camera:
 
     @staticmethod
     def threaded_render(cam: "Camera", world: Scene, samples_sqrt: int, seed: int = DEFAULT_SEED,
-                        ppm_path: str | None = "img.ppm", shard=None):
-        """camera.rs:223-352 on the GPU. Returns (framebuffer HxWx3 f64, stats)."""
+                        ppm_path: str | None = "img.ppm", shard=None, devices=None):
+        """camera.rs:223-352 on the GPUs of this node: the reference's pool takes every
+        core (camera.rs:253), this takes every visible GPU (`devices` None) or the
+        listed ones (rtw_threaded_render_multi). `shard` renders only those rows, on
+        one device (rtw_threaded_render). Returns (framebuffer HxWx3 f64, stats)."""
         sph, ns, mt, nm = world.flatten()
-        fb, st = render_flat(cam.raw, sph, ns, mt, nm, samples_sqrt, seed, shard)
+        if shard is not None:
+            fb, st = render_flat(cam.raw, sph, ns, mt, nm, samples_sqrt, seed, shard)
+        else:
+            fb, st = render_flat_multi(cam.raw, sph, ns, mt, nm, samples_sqrt, seed, devices)
         if ppm_path is not None and shard is None:
             write_ppm(ppm_path, fb)
         return fb, st
@@ -209,6 +215,19 @@ def render_flat_multi(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt, 
     check(lib.rtw_threaded_render_multi(C.byref(cam), sph, n_sph, mats, n_mats, samples_sqrt,
                                         capi.U128.of(seed), arr if devs else None, len(devs),
                                         fb.ctypes.data_as(C.POINTER(C.c_double)), C.byref(st)))
+    return fb, st
+
+
+def render_flat_multi_fast(cam: capi.Camera, sph, n_sph, mats, n_mats, samples_sqrt,
+                           seed=DEFAULT_SEED, devices=None):
+    """rtw_threaded_render_multi_fast: render_flat_multi in f32 fast mode."""
+    fb = np.zeros((cam.img_height, cam.img_width, 3), dtype=np.float32)
+    st = capi.Stats()
+    devs = list(devices or [])
+    arr = (C.c_int * max(1, len(devs)))(*devs)
+    check(lib.rtw_threaded_render_multi_fast(C.byref(cam), sph, n_sph, mats, n_mats, samples_sqrt,
+                                             capi.U128.of(seed), arr if devs else None, len(devs),
+                                             fb.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st)))
     return fb, st
 
 
@@ -331,6 +350,56 @@ class Session:
     def close(self):
         if self.h:
             lib.rtw_session_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Group:
+    """Device-resident multi-GPU renders (rtw_group_*): one session per device entry
+    (None = every visible device; an index may repeat), rows dealt cyclically, the
+    row tiles gathered on the root device (entry 0) by ncclGather over xGMI when the
+    entries are distinct GPUs (device copies otherwise) and un-permuted there into a
+    caller device buffer. Blocking renders."""
+
+    def __init__(self, devices=None, copy_gather: bool = False, rccl_always: bool = False):
+        self.h = C.c_void_p()
+        devs = list(devices or [])
+        arr = (C.c_int * max(1, len(devs)))(*devs)
+        flags = (capi.GROUP_COPY_GATHER if copy_gather else 0) | (capi.GROUP_RCCL_ALWAYS if rccl_always else 0)
+        check(lib.rtw_group_create(arr if devs else None, len(devs), flags, C.byref(self.h)))
+
+    def set_scene(self, sph, n_sph, mats, n_mats):
+        check(lib.rtw_group_set_scene(self.h, sph, n_sph, mats, n_mats))
+
+    def render(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int):
+        """The whole image into an H x W x 3 f64 buffer on the root device."""
+        check(lib.rtw_group_render(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
+                                   C.c_void_p(out_dev_ptr)))
+
+    def render_fast(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int):
+        """f32 fast mode into an H x W x 3 f32 buffer on the root device."""
+        check(lib.rtw_group_render_fast(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
+                                        C.c_void_p(out_dev_ptr)))
+
+    def stats(self):
+        """(total Stats, [per-entry Stats], info dict) of the last render."""
+        info = capi.GroupInfo()
+        check(lib.rtw_group_stats(self.h, None, None, 0, C.byref(info)))
+        total = capi.Stats()
+        per = (capi.Stats * max(1, info.n_entries))()
+        check(lib.rtw_group_stats(self.h, C.byref(total), per, max(1, info.n_entries), C.byref(info)))
+        d = info.as_dict()
+        d["gather"] = capi.GATHER_NAMES.get(info.gather, info.gather)
+        return total, [per[i] for i in range(info.n_entries)], d
+
+    def close(self):
+        if self.h:
+            lib.rtw_group_destroy(self.h)
             self.h = C.c_void_p()
 
     def __del__(self):

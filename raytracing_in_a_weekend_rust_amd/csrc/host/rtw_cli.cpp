@@ -5,7 +5,9 @@
 // Extra flags (the reference hard-codes or time-seeds these): --depth (MAX_DEPTH,
 // mod.rs:43), --seed (both XorShift::default seeds, mod.rs:67 / camera.rs:255),
 // --scene (the other builders of mod.rs), --out, --mode parity|fast (fast: the
-// f32 statistical mode, rtw_threaded_render_fast). --preview is accepted and
+// f32 statistical mode), --gpus N|LIST (N: the first N devices; LIST: comma-
+// separated device indices, repeats allowed; default: every visible device -- the
+// reference's pool takes every core, camera.rs:253). --preview is accepted and
 // ignored: the winit preview window (application/mod.rs) is out of scope.
 #include <chrono>
 #include <cstdio>
@@ -25,7 +27,36 @@ struct Config {  // main.rs:13-29
     unsigned __int128 seed = 0;
     bool seed_set = false;
     bool fast = false;
+    std::vector<int> devices;  // empty: every visible device
 };
+
+bool parse_u32(const char *s, uint32_t &v);
+
+// --gpus N (the first N devices) or a comma-separated device list ("0,0,1")
+bool parse_gpus(const char *s, std::vector<int> &out) {
+    if (!s || !*s) return false;
+    out.clear();
+    const bool list = std::strchr(s, ',') != nullptr;
+    std::string cur;
+    for (const char *p = s;; ++p) {
+        if (*p == ',' || !*p) {
+            uint32_t v = 0;
+            if (!parse_u32(cur.c_str(), v) || v > 65535) return false;
+            out.push_back(static_cast<int>(v));
+            cur.clear();
+            if (!*p) break;
+        } else {
+            cur.push_back(*p);
+        }
+    }
+    if (!list) {  // a count
+        const int n = out[0];
+        if (n == 0) return false;
+        out.clear();
+        for (int d = 0; d < n; ++d) out.push_back(d);
+    }
+    return true;
+}
 
 // Rust's str::parse::<usize>() (main.rs:37-39): an optional '+', then decimal
 // digits only (no whitespace, no sign '-', no base prefix).
@@ -82,6 +113,12 @@ Config parse_args(int argc, char **argv) {
             }
             c.fast = !std::strcmp(next, "fast");
         }
+        else if (a == "--gpus") {
+            if (!parse_gpus(next, c.devices)) {
+                std::fprintf(stderr, "Usage: --gpus <count> | <device,device,...>\n");
+                std::exit(1);
+            }
+        }
         else if (a == "--help") {
             std::printf("Use the application like this:\n");
             std::printf("\t-h --height\t:\tSet the height of the image\n");
@@ -93,6 +130,7 @@ Config parse_args(int argc, char **argv) {
             std::printf("\t--scene NAME\t:\tcomplex | simple | threads | super_simple | three_lambertian\n");
             std::printf("\t--out PATH\t:\tOutput PPM (reference: img.ppm)\n");
             std::printf("\t--mode M\t:\tparity (f64, bit-exact; default) | fast (f32, statistical)\n");
+            std::printf("\t--gpus N|LIST\t:\tthe first N GPUs, or device indices 0,1,.. (default: every GPU)\n");
             std::exit(0);
         }
     }
@@ -131,16 +169,17 @@ int main(int argc, char **argv) {
             rtw::FlatScene flat;
             b.world->flatten(flat);
             std::vector<float> f32(static_cast<size_t>(b.cam.width()) * b.cam.height() * 3);
-            int rc = rtw_threaded_render_fast(&b.cam.d, flat.spheres.data(),
-                                              static_cast<uint32_t>(flat.spheres.size()), flat.materials.data(),
-                                              static_cast<uint32_t>(flat.materials.size()), cfg.sample_sqrt,
-                                              seed, nullptr, f32.data(), &st);
+            int rc = rtw_threaded_render_multi_fast(
+                &b.cam.d, flat.spheres.data(), static_cast<uint32_t>(flat.spheres.size()), flat.materials.data(),
+                static_cast<uint32_t>(flat.materials.size()), cfg.sample_sqrt, seed,
+                cfg.devices.empty() ? nullptr : cfg.devices.data(), static_cast<uint32_t>(cfg.devices.size()),
+                f32.data(), &st);
             if (rc != RTW_OK) throw rtw::Error(rc, rtw_last_error());
             const std::vector<double> fb(f32.begin(), f32.end());
             rc = rtw_write_ppm(cfg.out.c_str(), fb.data(), b.cam.width(), b.cam.height());
             if (rc != RTW_OK) throw rtw::Error(rc, rtw_last_error());
         } else {
-            rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st);
+            rtw::Camera::threaded_render(b.cam, *b.world, cfg.sample_sqrt, seed, cfg.out.c_str(), &st, cfg.devices);
         }
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::printf("Finished succesfully: %s (%.3f s wall, kernel %.3f ms, %.1f Msamples/s, seed %s)\n",

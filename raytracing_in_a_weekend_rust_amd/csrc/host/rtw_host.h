@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "rtw_capi.h"
+#include "rtw_internal.h"  // rtw::Error
 
 namespace rtw {
 
@@ -141,12 +142,16 @@ struct Camera {
     uint32_t height() const { return d.img_height; }
     // camera.rs:422-450
     static std::vector<Vec3> offset_lattice(const Vec3 &dx, const Vec3 &dy, uint32_t num_layers);
-    // camera.rs:223-352: renders on the GPU and writes `ppm_path` ("img.ppm" in
-    // the reference); returns the f64 framebuffer (H*W*3). Throws on error.
+    // camera.rs:223-352: renders on the GPUs of this node and writes `ppm_path`
+    // ("img.ppm" in the reference); returns the f64 framebuffer (H*W*3). The
+    // reference's pool takes every core (camera.rs:253): an empty `devices` takes
+    // every visible GPU (rtw_threaded_render_multi), else the listed ones (an index
+    // may repeat). Throws on error.
     static std::vector<double> threaded_render(const Camera &cam, const Scene &world,
                                                uint32_t samples_sqrt, rtw_u128 seed,
                                                const char *ppm_path = "img.ppm",
-                                               rtw_stats *stats = nullptr);
+                                               rtw_stats *stats = nullptr,
+                                               const std::vector<int> &devices = {});
 };
 
 // ---- scenes (src/raytracing/mod.rs) ----
@@ -162,11 +167,5 @@ BuiltScene build_scene(const std::string &name, rtw_u128 seed, uint32_t h, uint3
 std::string format_ppm(const double *rgb, uint32_t w, uint32_t h);
 // the same text as the header followed by row-block chunks (no concatenation)
 std::vector<std::string> format_ppm_parts(const double *rgb, uint32_t w, uint32_t h);
-
-// Error carrying an RTW_E_* code (mapped to the C ABI's return value).
-struct Error : std::runtime_error {
-    int code;
-    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
-};
 
 }  // namespace rtw

@@ -95,7 +95,8 @@ RTW_HD float fmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 // a = d.d (hoisted), hb = oc.d, c = oc.oc - r*r, disc = hb*hb - a*c; roots
 // (-sq - hb)/a then (sq - hb)/a, the first inside [0.01, inf] (interval.rs:55-57).
 //
-// Exact early miss (no sqrt, no division; opt-in, RTW_EARLY_MISS): a ray
+// Exact early miss (no sqrt, no division; host analysis only -- on the device it
+// measured +0.3 %, a wave rarely skips as a whole, ab_early_miss_REJECTED.log): a ray
 // leaving a sphere it starts on or outside of (hb >= 0, c >= -1.6e-5 a). With
 // c >= 0, disc = RN(RN(hb^2) - RN(a c)) <= RN(hb^2) so sq <= hb and both roots
 // are <= 0. With -1.6e-5 a <= c < 0 (origin on the surface up to rounding) the
@@ -123,9 +124,6 @@ RTW_HD bool sphere_hit_f64(double ox, double oy, double oz, double dx, double dy
     const double ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
     const double hb = ocx * dx + ocy * dy + ocz * dz;
     const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rr;
-#ifdef RTW_EARLY_MISS  // measured +0.3 % on the device (a wave rarely skips as a whole): off
-    if (sphere_early_miss(hb, c, a)) return false;
-#endif
     const double disc = hb * hb - a * c;
     if (disc < 0.) return false;
     const double sq = __builtin_sqrt(disc);
@@ -138,10 +136,10 @@ RTW_HD bool sphere_hit_f64(double ox, double oy, double oz, double dx, double dy
 // (sphere_early_miss on the exact hb and c that sphere_hit_f64 computes, same
 // operations) cannot hit it at t >= 0.01, so the scan's minimum is the same
 // without it. Every bounce off a BVH sphere used to carry it as a candidate and an
-// exact f64 test (sqrt and both divisions). Returns the leaf id or 0xffff. Opt-in
-// on the device (RTW_SELF_SKIP): 37 % fewer candidates, but the wave's candidate
+// exact f64 test (sqrt and both divisions). Returns the leaf id or 0xffff. Host
+// analysis only: on the device, 37 % fewer candidates, but the wave's candidate
 // loop runs for its busiest lane's real candidates and the f64 check costs more
-// (+0.8 %, profiles/r02_misc/ab_self_skip_REJECTED.log); the host check uses it.
+// (+0.8 %, profiles/r02_misc/ab_self_skip_REJECTED.log).
 RTW_HD uint32_t self_skip(int prev, double ox, double oy, double oz, double dx, double dy, double dz,
                           double a, double cx, double cy, double cz, double rr) {
     const double ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
@@ -238,44 +236,18 @@ RTW_HD bool slab_hit(float nx, float ny, float nz, float fx, float fy, float fz,
 }
 
 // The four children's slab tests of one node as a hit mask (bit j = child j).
-// Opt-in RTW_PK_SLAB: the 24 plane FMAs as 12 v_pk_fma_f32 (children 0/1 and 2/3
-// in the halves of a register pair; each half the same IEEE fused multiply-add,
-// the same bits). Measured slower (parity +2.8 %, fast mode +5 %): a packed pair
-// occupies the SIMD as long as two plain f32 FMAs on gfx950, and the broadcast
-// ray constants take 9 more VGPRs (profiles/r02_misc/ab_pk_slab_REJECTED.log).
+// (The 24 plane FMAs as 12 v_pk_fma_f32 measured slower -- parity +2.8 %, fast mode
+// +5 %: a packed pair occupies the SIMD as long as two plain f32 FMAs on gfx950, and
+// the broadcast ray constants take 9 more VGPRs; profiles/r02_misc/ab_pk_slab_REJECTED.log.)
 template <typename F4>
 RTW_HD uint32_t slab_hit4(const F4 &nX, const F4 &nY, const F4 &nZ, const F4 &fX, const F4 &fY,
                           const F4 &fZ, const WalkRay &r, float U) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(RTW_PK_SLAB)
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
-    const f2 anx = {r.anx, r.anx}, any = {r.any, r.any}, anz = {r.anz, r.anz};
-    const f2 afx = {r.afx, r.afx}, afy = {r.afy, r.afy}, afz = {r.afz, r.afz};
-    uint32_t hit = 0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const f2 px = h ? f2{nX.z, nX.w} : f2{nX.x, nX.y}, py = h ? f2{nY.z, nY.w} : f2{nY.x, nY.y},
-                 pz = h ? f2{nZ.z, nZ.w} : f2{nZ.x, nZ.y};
-        const f2 qx = h ? f2{fX.z, fX.w} : f2{fX.x, fX.y}, qy = h ? f2{fY.z, fY.w} : f2{fY.x, fY.y},
-                 qz = h ? f2{fZ.z, fZ.w} : f2{fZ.x, fZ.y};
-        const f2 tnx = __builtin_elementwise_fma(px, ix, anx), tny = __builtin_elementwise_fma(py, iy, any),
-                 tnz = __builtin_elementwise_fma(pz, iz, anz);
-        const f2 tfx = __builtin_elementwise_fma(qx, ix, afx), tfy = __builtin_elementwise_fma(qy, iy, afy),
-                 tfz = __builtin_elementwise_fma(qz, iz, afz);
-        const float tn0 = fmax3(tnx.x, tny.x, tnz.x), tn1 = fmax3(tnx.y, tny.y, tnz.y);
-        const float tf0 = fmin3(tfx.x, tfy.x, tfz.x), tf1 = fmin3(tfx.y, tfy.y, tfz.y);
-        hit |= (fmaxf(tn0, r.tmin) <= fminf(tf0, U) ? 1u : 0u) << (2 * h);
-        hit |= (fmaxf(tn1, r.tmin) <= fminf(tf1, U) ? 2u : 0u) << (2 * h);
-    }
-    return hit;
-#else
     uint32_t hit = 0;
     hit |= slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, U) ? 1u : 0u;
     hit |= slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, U) ? 2u : 0u;
     hit |= slab_hit(nX.z, nY.z, nZ.z, fX.z, fY.z, fZ.z, r, U) ? 4u : 0u;
     hit |= slab_hit(nX.w, nY.w, nZ.w, fX.w, fY.w, fZ.w, r, U) ? 8u : 0u;
     return hit;
-#endif
 }
 
 // The pass-1 filter on leaf k; a kept sphere joins the candidate list (an
@@ -293,7 +265,7 @@ RTW_HD void leaf_test(const F4 *__restrict__ leaves, uint32_t k, const WalkRay &
     const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
     const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
     const float disc = fmaf(hb, hb, -cc);
-#if !defined(__HIP_DEVICE_COMPILE__) || defined(RTW_SELF_SKIP)
+#ifndef __HIP_DEVICE_COMPILE__  // the host check mirrors both candidate lists (tools/accel_check.cpp)
     ws.add_cand(k, !(disc < r.negG) && k != r.skip);  // kept unless the filter proves a miss
 #else
     ws.add_cand(k, !(disc < r.negG));  // kept unless the filter proves a miss

@@ -26,8 +26,7 @@
 // wave once the cursor is dry). The ray_color product att0*(att1*(...*leaf)) is
 // formed right-to-left from a per-path stack of sphere indices, so it associates
 // exactly as the recursion. rtw_park_leftover finishes any parked pixel nobody
-// claimed. The tile kernel (rtw_render_f64 + rtw_finish_parked, RTW_PERSIST=0)
-// stays for A/B and tests.
+// claimed.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -56,11 +55,7 @@ constexpr int kBlock = 256;  // 16 x 16 pixel tile, 4 waves
 // 768 threads = 3 waves per SIMD at the BVH kernel's ~150 VGPRs. (A 1024-thread
 // build fits 128 VGPRs with the per-lane LDS areas and few spills, but measured
 // slower: bulk throughput no better, drain groups slower.)
-#ifndef RTW_PBLOCK
-#define RTW_PBLOCK 768  // diagnostic builds: -DRTW_PBLOCK=512 (2 waves per SIMD)
-#endif
-constexpr int kPBlock = RTW_PBLOCK;
-constexpr int kTile = 16;
+constexpr int kPBlock = 768;
 constexpr int kChunk = 32;                // spheres per candidate mask (one bit per sphere)
 constexpr int kGroup = 8;                 // spheres per scalar-load group (8 x 16 B in SGPRs)
 constexpr size_t kLdsCap = 160 * 1024;    // dynamic LDS per workgroup (gfx950: 160 KiB)
@@ -83,7 +78,6 @@ constexpr uint32_t kHeavyPerBlockFullShort = 4;  // ... of fewer than 400 sample
 constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 samples) that park a
                                             // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
-constexpr uint32_t kCoopBlocks = 1024;  // persistent phase-2 grid (4 per CU)
 constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
 
 // Scene::hit strategies (one kernel instantiation each)
@@ -160,10 +154,6 @@ struct KParams {
     uint32_t drain_prio;        // draining waves' issue priority after the cursor phase (RTW_DRAIN_PRIO,
                                 // default 3; 0: unchanged)
     uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
-    uint32_t plist_thlog, plist_tx;  // camera-ray lists: log2 of the tile height (shard rows),
-                                     // tiles per row (tiles are 8 pixels wide)
-    uint32_t hot_tickets;       // waves holding one of the first hot_tickets pixels of the cost order
-                                // run at raised priority (0: off)
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
                                 // segments is parked before its first sample (0: off)
     uint64_t seed_lo, seed_hi;
@@ -183,10 +173,9 @@ struct KParams {
     uint64_t spill_stride;      // levels per column (lane-major; RTW_SPILL_LEVEL_MAJOR builds:
                                 // columns per level)
     uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
-    uint64_t *stamps_coop;      // RTW_STAMPS builds only: phase-2 waves [wave][8]
-    struct Parked *park;        // parked pixels (phase 1 -> rtw_finish_parked)
-    uint32_t *park_count;       // [0] parked, [1] phase-2 cursor
-    uint32_t *park_cursor;
+    struct Parked *park;        // parked pixels (cursor lanes -> drain groups)
+    uint32_t *park_count;       // parked pixels
+    uint32_t *park_cursor;      // the drain groups' next queue ticket
     U128 *seeds;                // per-pixel RNG children (persistent phase 1)
     uint32_t *diag;             // RTW_DIAG=1: per pixel {segments, clock/1024 at completion}
     uint32_t diag_ev;           // RTW_DIAG=2: then per pixel {hand-out, first park, first claim} clocks
@@ -194,8 +183,6 @@ struct KParams {
     uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base;
                                 // then per tile: its hot pixels
     uint32_t *pcost;            // per pixel: probe segments
-    uint4 *plist;               // per tile: candidate spheres of its camera rays (rtw_primary_lists)
-                                // or null
     uint32_t *cost_hist;        // [kCostBuckets] counts, then bucket write cursors
     uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
@@ -326,14 +313,9 @@ constexpr uint32_t kRegSlots = 8;
 // levels are contiguous (max_depth - kRegSlots u16 each), so a deep path dirties one
 // or two cache lines instead of one line per level -- the lanes of a persistent
 // wave push at different times, so the level-major layout's coalescing never
-// happened there, and its ~84 MB of level rows were written back line by line
-// (RTW_SPILL_LEVEL_MAJOR=1 builds keep it for A/B).
+// happened there, and its ~84 MB of level rows were written back line by line.
 __device__ __forceinline__ uint64_t spill_idx(uint32_t level, uint64_t col, uint64_t stride) {
-#ifdef RTW_SPILL_LEVEL_MAJOR
-    return static_cast<uint64_t>(level - kRegSlots) * stride + col;
-#else
     return col * stride + (level - kRegSlots);
-#endif
 }
 struct PathStack {
     uint64_t r0 = 0, r1 = 0;
@@ -410,13 +392,9 @@ struct SceneView {
     const uint16_t *nbr;
     float4 *end;  // first LDS float4 after the staged scene (kLds), else nullptr
 };
-// Shading records in LDS (default) or read from HBM through the caches
-// (RTW_SHADE_GLOBAL builds: 23 KB of LDS freed for more lanes per CU)
-#ifdef RTW_SHADE_GLOBAL
-constexpr size_t kShadeLds = 0;
-#else
+// Shading records in LDS (read from HBM through the caches instead, the 23 KB freed
+// for a fourth wave per SIMD: slower, profiles/r03_misc/ab_pblock1024_shadeglobal_REJECTED.log)
 constexpr size_t kShadeLds = sizeof(ShadeRec);
-#endif
 // inside-cut list entries (u16) in float4 units
 __host__ __device__ constexpr uint32_t nbr_f4(uint32_t n_nbr) { return (n_nbr + 7u) / 8u; }
 // BVH nodes in float4 units, padded to 32 B (the double4 records after them)
@@ -795,11 +773,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
             // one failed test every further TIR bounce inside the same S fails too, so
             // it is skipped (tir_no) until the path leaves the circle -- tracing on is
             // always exact, the forward only saves work
-#ifdef RTW_NO_TIR_CACHE  // A/B: test every TIR bounce
-            const bool skip = false;
-#else
             const bool skip = th.tir && best == tir_no;
-#endif
             tir_no = -1;
             if (!done && (th.lam || th.tir) && !skip) {
                 const uint32_t k = trap_forward(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
@@ -925,20 +899,13 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 
 // Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
 // exact candidates, the cut check; anything unproven falls back to the scan.
-// Camera-ray candidate list of a tile (rtw_primary_lists): count in the low 16
-// bits of x (kListNone: no list, walk), then up to kListMax sphere indices, 16 bits
-// each, from the high half of x on.
-constexpr uint32_t kListMax = 7;
-constexpr uint32_t kListNone = 0xffffu;
-__device__ __forceinline__ uint4 no_list() { return make_uint4(kListNone, 0u, 0u, 0u); }
-
 // kStride: the LDS scratch column stride (the workgroup size; a constant, so the
 // walk's pointer steps are immediates and hold no register)
 template <bool kLdsStack = false, uint32_t kStride = 0>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
-                                       double *sa_out = nullptr, uint4 pl = no_list()) {
+                                       double *sa_out = nullptr) {
     const double4 *__restrict__ sph = sv.sph;
     const float4 *__restrict__ nodes = sv.nodes;
     const float4 *__restrict__ leaves = sv.leaves;
@@ -957,43 +924,22 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
         }
         STAMP(5);  // 5: segment setup + always-spheres
         rtw_accel::WalkRay wr;
-        // a camera ray (prev < 0) of a tile with a list: its candidates are the list --
-        // every BVH sphere any camera ray of the tile can hit -- and there is no walk
-        const uint32_t lcount = pl.x & 0xffffu;
-        const bool listed = prev < 0 && lcount != kListNone;
         if (KP(n_node) == 0) {  // every sphere is an "always" sphere
-        } else if (!listed &&
-                   !rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
+        } else if (!rtw_accel::walk_setup(g.ox, g.oy, g.oz, g.ex, g.ey, g.ez, g.mo, g.sa, g.negG, wr)) {
             brute = true;
         } else {
             float U = best >= 0 ? rtw_accel::seed_cut(bt, g.sa) : INFINITY;
-#ifdef RTW_SELF_SKIP  // opt-in: measured +0.8 % (the wave's candidate loop is set by real candidates)
-            {  // the sphere the segment leaves is no candidate (rtw_accel.h self_skip)
-                const double4 S = sph[prev >= 0 ? prev : 0];
-                wr.skip = rtw_accel::self_skip(prev, ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w);
-            }
-#endif
             auto run = [&](auto &ws) {
-                bool walked = true;
-                if (listed) {  // the list's spheres become the candidates (index order irrelevant:
-                               // the exact loop keeps the (t, index) minimum)
-                    const uint32_t w[4] = {pl.x >> 16, pl.y, pl.z, pl.w};
-#pragma unroll
-                    for (uint32_t j = 0; j < kListMax; ++j) {
-                        const uint32_t id = (w[(j + 1u) >> 1] >> ((j & 1u) ? 0u : 16u)) & 0xffffu;
-                        ws.add_cand(j == 0 ? w[0] : id, j < lcount);
-                    }
-                } else {
-                    // the node walk at raised issue priority (cursor waves, kLdsStack): it
-                    // is a chain of dependent LDS round trips, so its wave should issue the
-                    // moment a load returns while the other waves' f64 code fills the gaps
-                    // (127.3 -> 124.9 ms; all of Scene::hit raised 125.9, the scatter
-                    // raised instead +1.9 %: profiles/r03_misc/ab_walk_prio.log). Cursor
-                    // waves run at priority 0 otherwise (hot waves: RTW_HOT_PRIO, off).
-                    if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(kWalkPrio);
-                    walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
-                    if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
-                }
+                // the node walk at raised issue priority (cursor waves, kLdsStack): it is
+                // a chain of dependent LDS round trips, so its wave should issue the
+                // moment a load returns while the other waves' f64 code fills the gaps
+                // (127.3 -> 124.9 ms; all of Scene::hit raised 125.9, the scatter raised
+                // instead +1.9 %: profiles/r03_misc/ab_walk_prio.log). Back to priority 0
+                // after it: every wave that walks with kLdsStack is a cursor wave at that
+                // point (a priority wave that joins the cursor runs as one).
+                if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(kWalkPrio);
+                const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
+                if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
                 STAMP(2);  // 2: BVH walk
                 if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
@@ -1015,7 +961,7 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
             if (!walked) {
                 brute = true;
             } else {
-                brute = !listed && !rtw_accel::cut_ok(U, best, bt, g.sa);  // a list cut nothing
+                brute = !rtw_accel::cut_ok(U, best, bt, g.sa);
             }
         }
     }
@@ -1084,72 +1030,6 @@ __device__ __forceinline__ SceneView stage_scene(const KParams &P, double4 *lds)
         v.end = reinterpret_cast<float4 *>(end);
     }
     return v;
-}
-
-// Phase 1: one lane per pixel (16x16 tiles). With a segment budget, pixels that
-// exceed it at a sample boundary park in P.park for rtw_finish_parked.
-template <bool kLds, int kMode>
-__global__ __launch_bounds__(kBlock) void rtw_render_f64(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
-    const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
-    const double4 *sph = sv.sph;
-
-    const uint32_t x = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
-    const uint32_t lr = blockIdx.y * kTile + (threadIdx.x / kTile);
-    Tally tl;
-    Stamps stp;
-
-    if (x < P.W && lr < P.n_rows) {
-        const uint32_t y = P.row_begin + lr * P.row_step;
-        PixelState ps;
-        ps.rng = child_of(jump_state(U128{P.seed_lo, P.seed_hi}, static_cast<uint64_t>(y) * P.W + x,
-                                     P.jump, P.jump_bits));
-        ps.k = 0;
-        ps.ar = ps.ag = ps.ab = 0.;
-        const uint64_t pix = static_cast<uint64_t>(lr) * P.W + x;  // spill column
-        auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a,
-                       int prev, double &bt) -> int {
-            if constexpr (kMode == kBvh) {
-                return bvh_hit(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp);
-            } else {
-                const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
-                return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
-            }
-        };
-        if (trace_samples(P, sv, x, y, P.spill, pix, ps, P.seg_budget, tl.seg, stp, hit)) {
-            const uint32_t slot = atomicAdd(P.park_count, 1u);
-            Parked q;
-            q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
-            q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
-            q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
-            P.park[slot] = q;
-            ++tl.parked;
-        } else {
-            write_pixel(P, x, lr, ps);
-        }
-    }
-
-#ifdef RTW_STAMPS
-    {  // max over lanes of each section sum -> one row per wave
-        const uint32_t lane = threadIdx.x & 63u;
-        uint64_t *row = P.stamps + (static_cast<uint64_t>(blockIdx.y) * gridDim.x * 4 + blockIdx.x * 4 + threadIdx.x / 64u) * kStampRow;
-        for (int k = 0; k < kStampSlots; ++k) {
-            uint64_t v = stp.acc[k];
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint64_t o = __shfl_xor(v, off);
-                v = v > o ? v : o;
-            }
-            if (lane == 0) row[k] = v;
-        }
-        uint64_t sm = tl.seg;
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(sm, off);
-            sm = sm > o ? sm : o;
-        }
-        if (lane == 0) row[14] = sm, row[15] = stamp_now();
-    }
-#endif
-    flush_tally(P, tl, true);
 }
 
 // Per-pixel RNG children (copy_reset, camera.rs:269-272) of the shard's pixels, in
@@ -1262,7 +1142,6 @@ __device__ __forceinline__ void shfl_min_step(double &bt, int &best, int off) {
 template <uint32_t kG>
 __device__ __forceinline__ void group_min(double &bt, int &best) {
     if constexpr (kG == 64) {
-#ifndef RTW_GROUP_MIN_FULL  // A/B: always the full reduction
         // most segments leave at most one lane of the group with a hit (the scan spreads
         // a segment's 1-2 candidates over the lanes, and a miss leaves none): that lane's
         // record is the minimum -- broadcast it (wave-uniform branch) instead of six
@@ -1277,7 +1156,6 @@ __device__ __forceinline__ void group_min(double &bt, int &best) {
             }
             return;
         }
-#endif
     }
     dpp_min_step<0xB1>(bt, best);   // quad_perm [1,0,3,2]
     dpp_min_step<0x4E>(bt, best);   // quad_perm [2,3,0,1]
@@ -1305,7 +1183,6 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
     const uint32_t info = shd[prev].nbr;
     if (info == rtw_accel::kNbrNone) return false;
     const uint32_t n = info & 0xffu;  // group-uniform, <= kMaxNbr < 16
-#ifndef RTW_INSIDE_SERIAL  // A/B: -DRTW_INSIDE_SERIAL tests S first, then the list
     // One pass for S and its list, side by side on the group's first n + 1 lanes (the
     // serial chain pays one sphere test instead of two in a row): lane j < n tests list
     // entry j as Sphere::hit does, lane n tests S as inside_far does -- the same
@@ -1363,7 +1240,6 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
         }
         return true;
     }
-#endif
     const double4 S = sph[prev];
     double t;
     if (!rtw_accel::inside_far(ox, oy, oz, dx, dy, dz, a, S.x, S.y, S.z, S.w * S.w, t)) return false;
@@ -1398,9 +1274,6 @@ template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, uint32_t fsh, const Parked &q,
                                                uint64_t col, Tally &tl, Stamps &stp) {
-#ifdef RTW_DIAG_NO_COOP  // register-pressure experiment only: the cursor path alone
-    return 0;
-#endif
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
@@ -1413,11 +1286,8 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     if (sub == 0) diag_event(P, static_cast<uint64_t>(P.n_rows) * P.W, pix, 2);
     // scenes of up to kCoopRegRec * kG spheres: the lane's pass-1 records live in
     // registers for the whole pixel (no LDS round trip on the serial chain)
-#ifndef RTW_COOP_REGREC
-#define RTW_COOP_REGREC 8  // 0: records always from LDS (register-pressure experiments)
-#endif
-    constexpr uint32_t kCoopRegRec = RTW_COOP_REGREC > 0 ? RTW_COOP_REGREC : 1;
-    const bool rec_in_regs = RTW_COOP_REGREC > 0 && n <= kCoopRegRec * kG;
+    constexpr uint32_t kCoopRegRec = 8;
+    const bool rec_in_regs = n <= kCoopRegRec * kG;
     float4 rr[kCoopRegRec];
     if (rec_in_regs) {
 #pragma unroll
@@ -1633,96 +1503,6 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
     if (mine) P.order_map[P.cost[t] + static_cast<uint32_t>(__popcll(m & ((1ull << r) - 1ull)))] = static_cast<uint32_t>(i);
 }
 
-// Camera-ray candidate lists. Every sample's first segment (get_ray, camera.rs:
-// 400-420) starts on the defocus disk o = look_from + ddu px + ddv py (|p| < 1) and
-// passes through a sample point s in its pixel's square (pixel00 + du (i + a) +
-// dv (j + b), a, b in [0, 1]: the lattice offsets lie inside it, camera.rs:422-450);
-// its points are (1 - t) o + t s for t >= 0.01 (interval.rs:55-57). In the camera
-// frame (u, v, depth along -w) a tile of pixels then bounds, for every t, the
-// lateral coordinates by t s_lo - |1 - t| R and t s_hi + |1 - t| R (R: the disk's
-// extent along the axis): a concave and a convex piecewise-linear bound, so over a
-// t interval their extremes sit at its ends. A BVH sphere is listed iff its padded
-// camera-frame box meets that region for some t whose depth reaches its depth slab.
-// The padding (2^-20 of the sphere's distance + radius, beyond the f64 Sphere::hit's
-// tangent-ray error ~2^-26.5 |oc|, plus an absolute slack) keeps the list a superset
-// of the spheres any camera ray of the tile can hit in the reference's f64
-// arithmetic. More than kListMax spheres, or a degenerate camera: no list (walk).
-struct PrimFrame {
-    double from[3], u[3], v[3], w[3];  // look_from and the camera basis (camera.rs:96-100)
-    double ru, rv, rz;                 // |o - look_from| along u, v, w (padded)
-    double eps;                        // absolute slack of every bound
-    uint32_t tw, th, tx, ty;           // tile width (pixels) and height (shard rows); tiles
-};
-__global__ __launch_bounds__(kBlock) void rtw_primary_lists(const KParams P, const PrimFrame F) {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= F.tx * F.ty) return;
-    const uint32_t tyi = t / F.tx, txi = t - tyi * F.tx;
-    const uint32_t x0 = txi * F.tw, x1 = min(x0 + F.tw, P.W) - 1u;
-    const uint32_t lr0 = tyi * F.th, lr1 = min(lr0 + F.th, P.n_rows) - 1u;
-    const uint32_t y0 = P.row_begin + lr0 * P.row_step, y1 = P.row_begin + lr1 * P.row_step;
-    const CamRef C(P);
-    // the tile's sample points relative to look_from, bounded along one axis e
-    double q[3];
-    for (int k = 0; k < 3; ++k)
-        q[k] = ((C(C.kP00 + k) + C(C.kDu + k) * static_cast<double>(x0)) + C(C.kDv + k) * static_cast<double>(y0)) -
-               F.from[k];
-    const double nx = static_cast<double>(x1 + 1u - x0), ny = static_cast<double>(y1 + 1u - y0);
-    auto range = [&](const double *e, double sgn, double &lo, double &hi) {
-        const double base = sgn * (q[0] * e[0] + q[1] * e[1] + q[2] * e[2]);
-        const double a = sgn * nx * (C(C.kDu) * e[0] + C(C.kDu + 1) * e[1] + C(C.kDu + 2) * e[2]);
-        const double b = sgn * ny * (C(C.kDv) * e[0] + C(C.kDv + 1) * e[1] + C(C.kDv + 2) * e[2]);
-        lo = base + fmin(a, 0.) + fmin(b, 0.) - F.eps;
-        hi = base + fmax(a, 0.) + fmax(b, 0.) + F.eps;
-    };
-    double ulo, uhi, vlo, vhi, zlo, zhi;
-    range(F.u, 1., ulo, uhi);
-    range(F.v, 1., vlo, vhi);
-    range(F.w, -1., zlo, zhi);  // depth along -w
-    uint4 out = make_uint4(kListNone, 0u, 0u, 0u);
-    if (zlo - F.rz > 0. && zhi < 1e300) {
-        const double inv_hi = 1. / (zhi + F.rz), inv_lo = 1. / (zlo - F.rz);
-        const double sU = fabs(ulo) + fabs(uhi) + F.ru, sV = fabs(vlo) + fabs(vhi) + F.rv;
-        uint32_t n = 0, w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-        const uint32_t nsph = P.n_sph, nal = P.n_always;
-        uint32_t ai = 0;
-        for (uint32_t k = 0; k < nsph; ++k) {  // wave-uniform
-            if (ai < nal && ld_const_u32(P.always, ai) == k) {  // tested before any walk anyway
-                ++ai;
-                continue;
-            }
-            const double4 S = P.sph[k];
-            const double r = fabs(S.w);
-            const double dx = S.x - F.from[0], dy = S.y - F.from[1], dz = S.z - F.from[2];
-            const double cu = dx * F.u[0] + dy * F.u[1] + dz * F.u[2];
-            const double cv = dx * F.v[0] + dy * F.v[1] + dz * F.v[2];
-            const double cz = -(dx * F.w[0] + dy * F.w[1] + dz * F.w[2]);
-            const double rp = r + 0x1p-20 * (fabs(dx) + fabs(dy) + fabs(dz) + r) + F.eps;
-            double t0 = (cz - rp - F.rz) * inv_hi, t1 = (cz + rp + F.rz) * inv_lo;
-            t0 = fmax(t0 - fabs(t0) * 1e-12, 0.01 * (1. - 1e-12));
-            t1 = t1 + fabs(t1) * 1e-12;
-            bool hit = t0 <= t1;
-            const double slack = 1e-12 * (t1 * (sU + sV) + (1. + t1) * (F.ru + F.rv)) + F.eps;
-            const double a0 = fabs(1. - t0), a1 = fabs(1. - t1);
-            const double lu = fmin(t0 * ulo - a0 * F.ru, t1 * ulo - a1 * F.ru) - slack;
-            const double hu = fmax(t0 * uhi + a0 * F.ru, t1 * uhi + a1 * F.ru) + slack;
-            const double lv = fmin(t0 * vlo - a0 * F.rv, t1 * vlo - a1 * F.rv) - slack;
-            const double hv = fmax(t0 * vhi + a0 * F.rv, t1 * vhi + a1 * F.rv) + slack;
-            hit = hit && cu - rp <= hu && cu + rp >= lu && cv - rp <= hv && cv + rp >= lv;
-            hit = hit || !(rp < 1e300) || !(fabs(cu) + fabs(cv) + fabs(cz) < 1e300);  // NaN / inf: keep
-            if (hit) {
-                const uint32_t id = k;
-                w0 = n == 0 ? id : w0, w1 = n == 1 ? (w1 & 0xffff0000u) | id : w1;
-                w1 = n == 2 ? (w1 & 0xffffu) | (id << 16) : w1;
-                w2 = n == 3 ? (w2 & 0xffff0000u) | id : w2, w2 = n == 4 ? (w2 & 0xffffu) | (id << 16) : w2;
-                w3 = n == 5 ? (w3 & 0xffff0000u) | id : w3, w3 = n == 6 ? (w3 & 0xffffu) | (id << 16) : w3;
-                ++n;
-            }
-        }
-        if (n <= kListMax) out = make_uint4(n | (w0 << 16), w1, w2, w3);
-    }
-    P.plist[t] = out;
-}
-
 // Phase 1, persistent form, with the heavy tail folded in. Every lane of a
 // cursor wave runs one pixel at a time and, when the pixel completes, takes the
 // next pixel of the shard from a global cursor (one atomic per wave per refill).
@@ -1764,12 +1544,11 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
 
     Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
     double seg_sa = 0.;  // sqrt(a) of the current segment (BVH hit), reused by the scatter
-    uint4 plst = no_list();  // the camera-ray candidate list of the lane's pixel's tile
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
             return bvh_hit<true, kThreads>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp, lane_stk + threadIdx.x,
-                                 &seg_sa, plst);
+                                 &seg_sa);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -1839,8 +1618,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
         uint32_t x = 0, lr = 0, pseg = 0;
         bool spec = false;  // spec_lds holds the state the lane's next unit vector draws from
-        bool hotpix = false;   // the lane's pixel is among the first hot_tickets of the cost order
-        bool wave_hot = false; // wave-uniform: the wave runs at raised priority for them
         uint64_t pix = 0;
         PixelState ps;
         Path p;
@@ -1860,7 +1637,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
 #endif
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
-                hotpix = ticket < P.hot_tickets;
                 if (ticket < npix) {
                     // hand-out order: by descending estimated cost (P.order_map,
                     // rtw_cost_probe), so the cheapest pixels fill the drain; else
@@ -1879,9 +1655,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     ps.rng = KP(seeds)[pix];
                     ps.k = 0;
                     diag_event(P, npix, pix, 0);
-#ifndef RTW_NO_PLIST
-                    if (const uint4 *pls = KP(plist)) plst = pls[(lr >> KP(plist_thlog)) * KP(plist_tx) + (x >> 3)];
-#endif
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
                     spec = false;
@@ -1907,17 +1680,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
             }
             dry = dry || __any(dry_now);  // wave-uniform
-            if (P.hot_tickets) {
-                // a wave holding one of the costliest pixels (the first hot_tickets of the
-                // cost order: the longest serial chains) issues at raised priority, so the
-                // chains that end the launch get more of their SIMD (RTW_HOT_PRIO)
-                const bool h = __any(!need && hotpix);
-                if (h != wave_hot) {
-                    wave_hot = h;
-                    if (h) __builtin_amdgcn_s_setprio(2);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-            }
             // endgame: once the cursor is dry and at most P.endgame pixels of the shard
             // are unfinished (about one per drain group), every lane parks its pixel
             // at its next sample boundary -- the last chains then run on a whole wave
@@ -2294,35 +2056,6 @@ __global__ __launch_bounds__(kBlock) void rtw_park_leftover(const KParams P) {
     flush_tally(P, tl, false);
 }
 
-// Phase 2 of the tile kernel: the parked pixels, kG lanes per pixel, in park order.
-template <bool kLds, uint32_t kG>
-__global__ __launch_bounds__(kBlock) void rtw_finish_parked(const KParams P) {
-    extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
-    const SceneView sv = stage_scene<kLds, kScanF32>(P, lds_sph);
-    const float4 *filt = stage_filt<kLds>(P, sv.end);
-    const uint32_t sub = threadIdx.x & (kG - 1u);
-    Tally tl;
-    Stamps stp;
-    uint32_t seg = 0;
-    for (;;) {
-        uint32_t item = 0;
-        if (sub == 0) item = atomicAdd(P.park_cursor, 1u);
-        item = __shfl(item, static_cast<int>(threadIdx.x & 63u & ~(kG - 1u)));
-        if (item >= *P.park_count) break;
-        const Parked q = P.park[item];
-        seg += coop_pixel<kG>(P, sv, filt, 0u, q, item, tl, stp);
-    }
-#ifdef RTW_STAMPS
-    if ((threadIdx.x & 63u) == 0) {  // diagnostic: per-wave rows after the tile kernel's
-        uint64_t *row = P.stamps_coop + (static_cast<uint64_t>(blockIdx.x) * (blockDim.x / 64u) + threadIdx.x / 64u) * kStampRow;
-        for (int k = 0; k < kStampSlots; ++k) row[k] = stp.acc[k];
-        row[14] = seg, row[15] = stamp_now();
-    }
-#endif
-    tl.seg = seg;
-    flush_tally(P, tl, false);
-}
-
 // Completeness latch, enqueued after every render: an image with fewer pixel
 // writes than pixels bumps the session's error word, which stays set until
 // rtw_session_stats reads it -- so a failed render is reported even when the
@@ -2382,7 +2115,6 @@ struct rtw_session {
     uint32_t *d_park_flag = nullptr; // per park slot publish flags
     uint32_t *d_order = nullptr, *d_cost = nullptr, *d_cost_hist = nullptr;  // cost-ordered hand-out
     uint32_t *d_pcost = nullptr;
-    uint4 *d_plist = nullptr;        // camera-ray candidate lists, one per tile (<= one per pixel)
     uint32_t *d_diag = nullptr;      // RTW_DIAG=1 per-pixel records
     size_t diag_bytes = 0, diag_n = 0;
     int n_cu = 0;
@@ -2714,11 +2446,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
     P.spill = s->d_spill;
     P.spill_b = s->d_spill ? s->d_spill + spill_need / (2 * sizeof(uint16_t)) : nullptr;
-#ifdef RTW_SPILL_LEVEL_MAJOR
-    P.spill_stride = spill_cols;
-#else
     P.spill_stride = cam->max_depth > kRegSlots ? cam->max_depth - kRegSlots : 0;
-#endif
     // park queue (one slot per pixel) and the per-pixel segment budget of phase 1
     const size_t npix_sh = static_cast<size_t>(sh.n_rows) * cam->img_width;
     if (npix_sh > s->park_cap) {
@@ -2728,16 +2456,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         dev_free(s->d_park);
         s->d_park = nullptr, s->park_cap = 0;
         dev_free(s->d_seeds), dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost);
-        dev_free(s->d_pcost), dev_free(s->d_plist);
+        dev_free(s->d_pcost);
         s->d_seeds = nullptr, s->d_park_flag = nullptr, s->d_order = nullptr, s->d_cost = nullptr;
-        s->d_pcost = nullptr, s->d_plist = nullptr;
+        s->d_pcost = nullptr;
         HIPCHECK(hipMalloc(&s->d_park, npix_sh * sizeof(Parked)));
         HIPCHECK(hipMalloc(&s->d_seeds, npix_sh * sizeof(U128)));
         HIPCHECK(hipMalloc(&s->d_park_flag, npix_sh * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_order, npix_sh * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_cost, 2 * npix_sh * sizeof(uint32_t)));  // 2 words per 8x8 tile
         HIPCHECK(hipMalloc(&s->d_pcost, npix_sh * sizeof(uint32_t)));
-        HIPCHECK(hipMalloc(&s->d_plist, npix_sh * sizeof(uint4)));
         s->park_cap = npix_sh;
     }
     P.park = s->d_park;
@@ -2765,8 +2492,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
 #ifdef RTW_STAMPS
     {
-        const size_t nt = static_cast<size_t>((P.W + kTile - 1) / kTile) * ((sh.n_rows + kTile - 1) / kTile) * 4;
-        const size_t nw = nt + static_cast<size_t>(kCoopBlocks) * (kBlock / 64);  // + phase-2 waves
+        // one row per wave of the persistent launch (one workgroup per CU)
+        const size_t nw = static_cast<size_t>(s->n_cu > 0 ? s->n_cu : 256) * (kPBlock / 64);
         static uint64_t *d_st = nullptr;
         static size_t cap = 0;
         if (nw * kStampRow * 8 > cap) {
@@ -2776,7 +2503,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         }
         HIPCHECK(hipMemset(d_st, 0, nw * kStampRow * 8));
         P.stamps = d_st;
-        P.stamps_coop = d_st + nt * kStampRow;
         stamp_buf() = d_st;
         stamp_n() = nw;
     }
@@ -2808,19 +2534,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     HIPCHECK(hipSetDevice(s->device));
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
     order_after_last(s, st);
-    const dim3 grid((P.W + kTile - 1) / kTile, (P.n_rows + kTile - 1) / kTile);
     // Scene::hit strategy: RTW_ACCEL=0 f64 scan, 1 filtered scan, 2 BVH (default
     // when the scene is eligible); A/B and tests only -- results are identical.
     int mode = s->has_bvh ? kBvh : kScanF32;
     if (const char *e = std::getenv("RTW_ACCEL")) mode = std::atoi(e);
     if (mode == kBvh && !s->has_bvh) mode = kScanF32;
     if (mode < kScanF64 || mode > kBvh) mode = kScanF32;
-    // phase 1: persistent per-lane refill (default) or one tile per workgroup (RTW_PERSIST=0)
-    bool persist = true;
-    if (const char *e = std::getenv("RTW_PERSIST")) persist = std::atoi(e) != 0;
     size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh, P.n_nbr);
     // pass-1 records for the coop groups (BVH scenes read them from the leaves)
-    if (persist && mode != kBvh) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);
+    if (mode != kBvh) lds += static_cast<size_t>(P.n_sph) * sizeof(float4);
     const bool use_lds = lds <= kLdsCap;
     if (!use_lds) lds = 0;
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
@@ -2829,7 +2551,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.order = 2;
     if (const char *e = std::getenv("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
     uint32_t grid_p = 0;
-    if (P.n_rows && persist) {
+    if (P.n_rows) {
         const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
         // per-pixel seeds (a separate launch: measured 0.7 ms faster than deriving
         // them inside the LDS-heavy cost probe)
@@ -2837,44 +2559,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((seed_threads + kBlock - 1) / kBlock)),
                            dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
-        // camera-ray candidate lists (rtw_primary_lists), BVH scenes: 8-pixel-wide
-        // tiles of 8 image rows' worth of the shard (a row shard's rows are row_step
-        // apart).
-        P.plist = nullptr;
-        // Opt-in (RTW_PLIST=1): measured 1.4 % slower at N=1 (profiles/r03_misc/
-        // ab_camera_ray_lists_REJECTED.log). Camera rays walk no shorter than others
-        // (5.46 visits vs 5.39), so the wave's walk -- the max over its lanes -- drops
-        // only 8.7 % without them (walk_diag_camera_rays.log), and the lists' exact
-        // tests, the fill and the list kernel eat that.
-        bool plist_on = false;
-        if (const char *e = std::getenv("RTW_PLIST")) plist_on = std::atoi(e) != 0;
-        plist_on = plist_on && mode == kBvh && P.max_depth > 0 && s->n_node > 0;
-        if (plist_on) {
-            PrimFrame F{};
-            auto cp3 = [](double *d, const rtw_vec3 &v) { d[0] = v.x, d[1] = v.y, d[2] = v.z; };
-            cp3(F.from, cam->look_from), cp3(F.u, cam->u), cp3(F.v, cam->v), cp3(F.w, cam->w);
-            auto dotv = [](const rtw_vec3 &a, const double *b) { return a.x * b[0] + a.y * b[1] + a.z * b[2]; };
-            const bool disk = cam->defocus_angle > 0.;
-            const double pad = 1. + 1e-9;
-            F.ru = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.u)) + std::fabs(dotv(cam->defocus_disk_v, F.u))) * pad : 0.;
-            F.rv = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.v)) + std::fabs(dotv(cam->defocus_disk_v, F.v))) * pad : 0.;
-            F.rz = disk ? (std::fabs(dotv(cam->defocus_disk_u, F.w)) + std::fabs(dotv(cam->defocus_disk_v, F.w))) * pad : 0.;
-            auto nrm = [](const rtw_vec3 &v) { return std::fabs(v.x) + std::fabs(v.y) + std::fabs(v.z); };
-            F.eps = 1e-9 * (nrm(cam->look_from) + nrm(cam->pixel00) + (cam->img_width + 1.) * nrm(cam->pixel_delta_u) +
-                            (cam->img_height + 1.) * nrm(cam->pixel_delta_v) + F.ru + F.rv + F.rz + 1.);
-            F.tw = 8;
-            F.th = std::max(1u, 8u / std::max(1u, P.row_step));  // 8, 4, 2 or 1: a power of two
-            if (F.th & (F.th - 1u)) F.th = 1u;
-            F.tx = (P.W + F.tw - 1) / F.tw;
-            F.ty = (P.n_rows + F.th - 1) / F.th;
-            if (std::isfinite(F.eps) && static_cast<uint64_t>(F.tx) * F.ty <= npix) {
-                P.plist = s->d_plist;
-                P.plist_thlog = static_cast<uint32_t>(__builtin_ctz(F.th)), P.plist_tx = F.tx;
-                hipLaunchKernelGGL(rtw_primary_lists, dim3((F.tx * F.ty + kBlock - 1) / kBlock), dim3(kBlock), 0, st, P,
-                                   F);
-                HIPCHECK(hipGetLastError());
-            }
-        }
         // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
         // bottom-up, 0 row-major
         P.order_map = nullptr;
@@ -3002,8 +2686,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
         if (const char *e = std::getenv("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (const char *e = std::getenv("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
-        if (const char *e = std::getenv("RTW_HOT_PRIO"))  // percent of the shard's pixels
-            P.hot_tickets = P.order_map ? static_cast<uint32_t>(std::atof(e) / 100. * static_cast<double>(npix)) : 0u;
         if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
@@ -3017,35 +2699,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         if (lds2 <= kLdsCap) hipLaunchKernelGGL((rtw_park_leftover<true, 64>), grid_l, dim3(kBlock), lds2, st, P);
         else hipLaunchKernelGGL((rtw_park_leftover<false, 64>), grid_l, dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
-    } else if (P.n_rows) {
-#define RTW_LAUNCH(L, M) hipLaunchKernelGGL((rtw_render_f64<L, M>), grid, dim3(kBlock), lds, st, P)
-        if (use_lds) {
-            if (mode == kBvh) RTW_LAUNCH(true, kBvh);
-            else if (mode == kScanF32) RTW_LAUNCH(true, kScanF32);
-            else RTW_LAUNCH(true, kScanF64);
-        } else {
-            if (mode == kBvh) RTW_LAUNCH(false, kBvh);
-            else if (mode == kScanF32) RTW_LAUNCH(false, kScanF32);
-            else RTW_LAUNCH(false, kScanF64);
-        }
-#undef RTW_LAUNCH
-        HIPCHECK(hipGetLastError());
-    }
-    if (P.n_rows && !persist) {
-        if (P.seg_budget != 0xffffffffu) {  // phase 2 of the tile kernel: parked pixels, coop groups
-            const size_t lds2 = lds_bytes_for(P.n_sph, 0, 0, false) + static_cast<size_t>(P.n_sph) * sizeof(float4);
-            const dim3 grid2(kCoopBlocks);
-            int g = 16;
-            if (const char *e = std::getenv("RTW_COOP")) g = std::atoi(e);
-            if (lds2 <= kLdsCap) {
-                if (g == 64) hipLaunchKernelGGL((rtw_finish_parked<true, 64>), grid2, dim3(kBlock), lds2, st, P);
-                else hipLaunchKernelGGL((rtw_finish_parked<true, 16>), grid2, dim3(kBlock), lds2, st, P);
-            } else {
-                if (g == 64) hipLaunchKernelGGL((rtw_finish_parked<false, 64>), grid2, dim3(kBlock), 0, st, P);
-                else hipLaunchKernelGGL((rtw_finish_parked<false, 16>), grid2, dim3(kBlock), 0, st, P);
-            }
-            HIPCHECK(hipGetLastError());
-        }
     }
     hipLaunchKernelGGL(rtw_latch_check<uint32_t>, dim3(1), dim3(64), 0, st,
                        static_cast<const uint32_t *>(P.pixels_done),
@@ -3057,12 +2710,12 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     s->last = rtw_stats{};
     s->last.pixels = static_cast<uint64_t>(P.n_rows) * P.W;
     s->last.samples = s->last.pixels * P.n_off;
-    s->last.grid_blocks = persist ? grid_p : grid.x * grid.y;
-    s->last.block_threads = kBlock;
+    s->last.grid_blocks = grid_p;
+    s->last.block_threads = kPBlock;
     s->last.accel = static_cast<uint32_t>(mode);
     s->last.lds_bytes = static_cast<uint32_t>(lds);
     s->last_fast = false;
-    s->main_ev = P.n_rows && persist;
+    s->main_ev = P.n_rows != 0;
 }
 
 // f32 fast mode (rtw_fast.hip): same camera, shard and validation as render().
@@ -3305,26 +2958,11 @@ int threaded(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_sphere
     RTW_GUARD_END
 }
 
-// Counters of several shards of one image: sums, the slowest render's time.
-static void add_stats(rtw_stats &a, const rtw_stats &b, bool first) {
-    if (first) {
-        a = b;
-        return;
-    }
-    a.pixels += b.pixels, a.samples += b.samples, a.segments += b.segments;
-    a.sphere_tests += b.sphere_tests, a.wave_iterations += b.wave_iterations;
-    a.exact_tests += b.exact_tests, a.exact_wave_iterations += b.exact_wave_iterations;
-    a.kernel_ms = std::max(a.kernel_ms, b.kernel_ms);
-    a.node_visits += b.node_visits, a.brute_segments += b.brute_segments;
-    a.parked_pixels += b.parked_pixels, a.inside_segments += b.inside_segments;
-    a.trap_segments += b.trap_segments, a.guard_exits += b.guard_exits;
-    a.leftover_pixels += b.leftover_pixels;
-}
-
-// rtw_threaded_render_multi: one host thread per device entry, rows r = i mod n.
+// rtw_threaded_render_multi(_fast): one host thread per device entry, rows r = i mod n.
+template <typename T, typename Run>
 static int threaded_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres, const rtw_material *mats,
-                   uint32_t n_mats, uint32_t samples_sqrt, rtw_u128 seed, const int *devices, uint32_t n_devices,
-                   double *out_rgb, rtw_stats *stats) {
+                          uint32_t n_mats, const int *devices, uint32_t n_devices, T *out_rgb, rtw_stats *stats,
+                          Run run) {
     if (!cam || !out_rgb || (n_devices && !devices)) return rtw::set_error("null argument"), RTW_E_ARG;
     std::lock_guard<std::mutex> lock(g_multi_mu);
     RTW_GUARD_BEGIN
@@ -3356,9 +2994,9 @@ static int threaded_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint
                 HIPCHECK(hipSetDevice(s->device));
                 set_scene(s, spheres, n_spheres, mats, n_mats);
                 const rtw_shard sh{i, n, (H - i + n - 1) / n, 0};
-                const size_t row = static_cast<size_t>(W) * 3 * sizeof(double);
-                double *d_out = static_cast<double *>(session_out(s, sh.n_rows * row));
-                render(s, cam, samples_sqrt, seed, &sh, d_out, s->own);
+                const size_t row = static_cast<size_t>(W) * 3 * sizeof(T);
+                T *d_out = static_cast<T *>(session_out(s, sh.n_rows * row));
+                run(s, &sh, d_out, s->own);
                 collect(s);
                 // the gather: tile row k -> image row i + k n, one strided copy
                 HIPCHECK(hipMemcpy2D(out_rgb + static_cast<size_t>(i) * W * 3, n * row, d_out, row, row, sh.n_rows,
@@ -3374,7 +3012,7 @@ static int threaded_multi(const rtw_camera *cam, const rtw_sphere *spheres, uint
         if (e) std::rethrow_exception(e);
     if (stats) {
         rtw_stats acc{};
-        for (uint32_t i = 0; i < n; ++i) add_stats(acc, st[i], i == 0);
+        for (uint32_t i = 0; i < n; ++i) rtw::add_stats(acc, st[i], i == 0);
         *stats = acc;
     }
     return RTW_OK;
@@ -3407,7 +3045,7 @@ int rtw_session_destroy(rtw_session *s) {
     dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
-    dev_free(s->d_pcost), dev_free(s->d_plist), dev_free(s->d_err);
+    dev_free(s->d_pcost), dev_free(s->d_err);
     dev_free(s->d_fcursor), dev_free(s->d_fcount);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
@@ -3480,8 +3118,20 @@ int rtw_threaded_render_multi(const rtw_camera *cam, const rtw_sphere *spheres, 
                               const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
                               rtw_u128 seed, const int *devices, uint32_t n_devices, double *out_rgb,
                               rtw_stats *stats) {
-    return threaded_multi(cam, spheres, n_spheres, mats, n_mats, samples_sqrt, seed, devices, n_devices, out_rgb,
-                          stats);
+    return threaded_multi(cam, spheres, n_spheres, mats, n_mats, devices, n_devices, out_rgb, stats,
+                          [&](rtw_session *s, const rtw_shard *sh, double *d, hipStream_t st) {
+                              render(s, cam, samples_sqrt, seed, sh, d, st);
+                          });
+}
+
+int rtw_threaded_render_multi_fast(const rtw_camera *cam, const rtw_sphere *spheres, uint32_t n_spheres,
+                                   const rtw_material *mats, uint32_t n_mats, uint32_t samples_sqrt,
+                                   rtw_u128 seed, const int *devices, uint32_t n_devices, float *out_rgb,
+                                   rtw_stats *stats) {
+    return threaded_multi(cam, spheres, n_spheres, mats, n_mats, devices, n_devices, out_rgb, stats,
+                          [&](rtw_session *s, const rtw_shard *sh, float *d, hipStream_t st) {
+                              render_fast(s, cam, samples_sqrt, seed, sh, d, st);
+                          });
 }
 
 int rtw_shutdown(void) {

@@ -18,6 +18,17 @@ drives the same code over gloo with the oracle standing in for the GPU render.
 from __future__ import annotations
 
 
+def group_devices(n: int, visible: int):
+    """Device entries of a one-process N-GPU group (bench.py --gpus N without
+    torchrun): the first N devices, or -- on a box with fewer GPUs -- the visible
+    ones repeated round-robin (entries then share a GPU: a rehearsal of the N-way
+    split and its gather, not a scaling point). Returns (devices, repeated)."""
+    if n < 1 or visible < 1:
+        raise ValueError(f"need n >= 1 and a visible device (n={n}, visible={visible})")
+    devs = [i % visible for i in range(n)]
+    return devs, n > visible
+
+
 def frame_seed(seed: int, frame: int) -> int:
     """Render seed of frame `frame` of a multi-frame job. The reference seeds every
     render from the wall clock in ms (random.rs:16-22, camera.rs:255), so renders

@@ -32,6 +32,24 @@ def test_cli_parity_ppm_matches_oracle(tmp_path):
     assert ppm == orc.format_ppm(ref)
 
 
+@pytest.mark.parametrize("gpus", ["0,0", "1", "0,0,0"])
+def test_cli_parity_ppm_matches_oracle_on_device_lists(tmp_path, gpus):
+    """--gpus: the rows dealt over the listed devices (rtw_threaded_render_multi),
+    the same PPM as the one-device render and the oracle."""
+    ppm, stdout = run_cli(tmp_path, "--gpus", gpus)
+    assert "Finished succesfully" in stdout
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 18, 32, 12)
+    ref, _ = orc.render(cam.raw, sph, n, mt, nm, 3, SEED)
+    assert ppm == orc.format_ppm(ref)
+
+
+def test_cli_fast_mode_on_device_list(tmp_path):
+    ppm, _ = run_cli(tmp_path, "--mode", "fast", "--gpus", "0,0")
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 18, 32, 12)
+    fb, _ = rtw.render_flat_fast(cam.raw, sph, n, mt, nm, 3, SEED)
+    assert ppm == rtw.format_ppm(fb.astype(np.float64))
+
+
 def test_cli_fast_mode_ppm(tmp_path):
     ppm, _ = run_cli(tmp_path, "--mode", "fast")
     head, body = ppm.split(b"\n", 3)[:3], ppm.split(b"\n", 3)[3]
@@ -46,3 +64,9 @@ def test_cli_fast_mode_ppm(tmp_path):
 def test_cli_rejects_bad_mode(tmp_path):
     r = subprocess.run([CLI, "--mode", "turbo"], capture_output=True, text=True, timeout=30)
     assert r.returncode == 1 and "--mode" in r.stderr
+
+
+@pytest.mark.parametrize("bad", ["x", "0", "1,,2", "-1", ""])
+def test_cli_rejects_bad_gpus(bad):
+    r = subprocess.run([CLI, "--gpus", bad], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 1 and "--gpus" in r.stderr

@@ -190,11 +190,10 @@ def test_filter_stress_scenes():
         assert_same(fb, ref, st, seg)
 
 
-STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x budget x group
+STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, variant): Scene::hit strategy x budget x schedule
     ("0", "0", "16"), ("1", "0", "16"), ("2", "0", "16"),  # f64 scan / filtered scan / BVH
-    ("2", "0.01", "16"), ("2", "0.01", "64"),  # park every pixel after its first sample
+    ("2", "0.01", "coopg16"), ("2", "0.01", "64"),  # park every pixel after its first sample
     ("2", "1.5", "16"), ("1", "2", "64"),      # park the heavier pixels
-    ("2", "1.5", "tile"), ("0", "0", "tile"),  # one-tile-per-workgroup phase 1 (RTW_PERSIST=0)
     ("2", "0.3", "heavy0"), ("2", "2", "heavy3"),  # persistent: drain by plain waves / 3 priority waves
     ("2", "0", "rate1"),                        # rate-based parking of nearly every pixel
     ("2", "0", "order0"), ("2", "0", "order1"),  # row-major / bottom-up hand-out (default: by cost)
@@ -204,7 +203,6 @@ STRATEGIES = [  # (RTW_ACCEL, RTW_BUDGET_X, RTW_COOP): Scene::hit strategy x bud
     ("2", "0", "endgame_coopg16"),
     ("2", "0", "probe2"), ("2", "0.3", "probe3"),  # cost probe on one pixel per 2x2 / 3x3 block
     ("2", "0", "prepark"), ("2", "0", "drainprio0"),  # probe-hot pixels parked at once; drain at prio 0
-    ("2", "0", "plist1"), ("2", "0.3", "plist1"),  # camera rays take per-tile candidate lists (opt-in)
 ]
 
 
@@ -214,8 +212,6 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     pixels into the cooperative kernel) gives the oracle's image bit-for-bit."""
     monkeypatch.setenv("RTW_ACCEL", accel)
     monkeypatch.setenv("RTW_BUDGET_X", budget)
-    monkeypatch.setenv("RTW_COOP", coop if coop in ("16", "64") else "16")
-    monkeypatch.setenv("RTW_PERSIST", "0" if coop == "tile" else "1")
     monkeypatch.setenv("RTW_HEAVY", {"heavy0": "0", "heavy3": "3"}.get(coop, "1"))
     monkeypatch.setenv("RTW_RATE_X", "1" if coop == "rate1" else "8")
     monkeypatch.setenv("RTW_RATE_K", "2" if coop == "rate1" else "16")
@@ -227,7 +223,6 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
     monkeypatch.setenv("RTW_PROBE_SUB", coop[5:] if coop.startswith("probe") else "1")
     monkeypatch.setenv("RTW_PREPARK", "4" if coop == "prepark" else "0")
     monkeypatch.setenv("RTW_DRAIN_PRIO", "0" if coop == "drainprio0" else "3")
-    monkeypatch.setenv("RTW_PLIST", "1" if coop == "plist1" else "0")
     if coop == "endgame_coopg16":
         monkeypatch.setenv("RTW_COOPG", "16")
     cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
@@ -253,7 +248,7 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
 def test_strategies_on_stress_and_deep_scenes(monkeypatch, tmp_path, accel, budget, coop):
     monkeypatch.setenv("RTW_ACCEL", accel)
     monkeypatch.setenv("RTW_BUDGET_X", budget)
-    monkeypatch.setenv("RTW_COOP", coop)
+    monkeypatch.setenv("RTW_COOPG", coop)
     test_filter_stress_scenes()
     _deep_closed_sphere()
     _escaping_mirrors()
@@ -524,14 +519,12 @@ def test_shutdown_frees_and_recreates_sessions():
     rtw.shutdown()
 
 
-@pytest.mark.parametrize("plist", ["1", "0"])
-def test_camera_ray_lists_on_frustum_edges(monkeypatch, plist):
-    """Camera rays take their tile's candidate list (rtw_primary_lists) instead of the
-    walk. A scene built to sit on the lists' bounds: spheres tangent to pixel and
-    tile frusta, grazing the defocus cone, straddling the focus plane, behind and
-    around the camera, a camera inside a sphere, and a sphere cluster wider than a
-    list (no list: walk). Bit-exact with lists on and off."""
-    monkeypatch.setenv("RTW_PLIST", plist)
+def test_camera_rays_on_frustum_edges():
+    """Camera rays through a scene built on pixel-frustum edges: spheres tangent to
+    pixel and tile frusta, grazing the defocus cone, straddling the focus plane,
+    behind and around the camera, a camera inside a sphere, and a tight sphere
+    cluster (once the bounds of the rejected per-tile camera-ray candidate lists,
+    kept as a walk stress scene). Bit-exact."""
     rng = np.random.default_rng(23)
     world = rtw.SceneBuilder()
     lam = rtw.Lambertian((0.6, 0.5, 0.4))

@@ -217,7 +217,7 @@ def test_reference_asserts_become_error_codes():
 
 
 def test_abi_version_and_build_id():
-    assert capi.lib.rtw_abi_version() == capi.ABI_VERSION == 6
+    assert capi.lib.rtw_abi_version() == capi.ABI_VERSION == 7
     bid = rtw.build_id()
     assert re.fullmatch(r"[0-9a-f]{12}-[0-9a-f]{4}", bid), bid
     assert bid.encode() in capi.lib.rtw_version()

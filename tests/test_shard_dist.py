@@ -110,3 +110,28 @@ def test_frame_per_rank_weak_scaling(tmp_path):
         ref, _ = orc.render(cam, sph, n, mat, n, S, shard.frame_seed(SEED, f), nthreads=2)
         assert np.array_equal(got[f], ref)
     assert not np.array_equal(got[0], got[1])  # independent frames, not replicas
+
+
+def test_group_devices_for_plain_bench_command():
+    """bench.py --gpus N without a launcher: the first N devices, or the visible ones
+    repeated round-robin (labelled: not a scaling point)."""
+    assert shard.group_devices(8, 8) == ([0, 1, 2, 3, 4, 5, 6, 7], False)
+    assert shard.group_devices(2, 8) == ([0, 1], False)
+    assert shard.group_devices(4, 1) == ([0, 0, 0, 0], True)
+    assert shard.group_devices(3, 2) == ([0, 1, 0], True)
+    with pytest.raises(ValueError):
+        shard.group_devices(2, 0)
+
+
+def test_group_rows_match_rank_rows():
+    """An rtw_group entry i renders the rows rank i of a torchrun split renders
+    (rows_of), into tiles padded to rows_max: the un-permute maps tile row k of
+    entry i to image row i + k*N, covering every row once."""
+    for world, h in [(1, 5), (2, 675), (3, 7), (8, 675), (5, 3)]:
+        n = min(world, h)
+        seen = []
+        for i in range(n):
+            b, step, rows = shard.rows_of(i, n, h)
+            assert rows <= shard.rows_max(n, h)
+            seen += [b + k * step for k in range(rows)]
+        assert sorted(seen) == list(range(h))
