@@ -81,7 +81,11 @@ oracle:
 stamps: $(OUT)/librtw_stamps.so
 $(OUT)/rtw_render_stamps.o: $(SRC)/rtw_render.hip include/rtw_capi.h $(SRC)/host/rtw_host.h
 	$(HIPCC) $(HIPFLAGS) -DRTW_STAMPS -c $< -o $@
-$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_group.o $(OUT)/rtw_host.o $(OUT)/rtw_accel_build.o
+# its own host object: rtw_build_id() carries "+stamps" (the diagnostic
+# library must not report the default build's id)
+$(OUT)/rtw_host_stamps.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h $(OUT)/rtw_build_id.h
+	$(CXX) $(CXXFLAGS) -I$(OUT) '-DRTW_BUILD_VARIANT="+stamps"' -c $< -o $@
+$(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_group.o $(OUT)/rtw_host_stamps.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
 asm: $(SRC)/rtw_render.hip

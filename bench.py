@@ -262,6 +262,19 @@ def available_parallelism():
     return n, how
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), as SURVEY 8(d) asks."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
     """Oracle (C restatement) on a row sample, ref-faithful scheduler: one job per
     pixel pulled by `threads` workers, dyn dispatch + Arc-refcount traffic as in
@@ -289,7 +302,7 @@ def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
             "sample": f"rows 0::{stride} ({n_rows} rows x {cam.img_width} px x {s * s} spp, "
                       f"{samples / 1e6:.1f} Msamples) of the same image, {dt:.1f} s, "
                       f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible",
-            "threads_rule": how,
+            "threads_rule": how, "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "clean_scheduler": {"value": samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
                                 "sample": f"rows 0::{stride} ({n_rows} rows), {c_dt:.1f} s, row jobs, "
                                           "direct calls"}}
