@@ -495,6 +495,8 @@ def test_multi_device_abi_matches_single_device(devices):
     fb, mst = rtw.render_flat_multi(cam.raw, sph, n, mt, nm, 3, SEED, devices=devices)
     assert np.array_equal(fb, ref)
     assert mst.segments == st.segments and mst.pixels == 61 * 96 and mst.samples == st.samples
+    # merged times: the slowest entry's main kernel and whole render
+    assert 0 < mst.main_kernel_ms <= mst.kernel_ms
 
 
 def test_multi_device_more_entries_than_rows():

@@ -44,6 +44,9 @@ __global__ __launch_bounds__(64) void bench(uint32_t active, uint64_t *cycles, d
                 f3 = __builtin_fmaf(f3, mf, cf), f4 = __builtin_fmaf(f4, mf, cf), f5 = __builtin_fmaf(f5, mf, cf);
                 f6 = __builtin_fmaf(f6, mf, cf), f7 = __builtin_fmaf(f7, mf, cf);
                 asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3), "+v"(f4), "+v"(f5), "+v"(f6), "+v"(f7));
+            } else if constexpr (kKind == 3) {  // ONE dependent f64 FMA chain (a drain's serial shape)
+                a0 = __builtin_fma(a0, m, c);
+                asm volatile("" : "+v"(a0));
             } else {  // u128 xorshift(23,17,26) on 4 u32 limbs: an integer chain (8 ops)
                 x0 ^= x0 << 23, x1 ^= x1 >> 17, x2 ^= x2 << 26, x3 ^= x3 >> 5;
                 asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
@@ -83,7 +86,7 @@ int main() {
     int n_cu = 0;
     CK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0));
     if (run<0>("f64 fma (8 chains)", 8, n_cu) || run<1>("f32 fma (8 chains)", 8, n_cu) ||
-        run<2>("u32 shift-xor (4x2)", 8, n_cu))
+        run<2>("u32 shift-xor (4x2)", 8, n_cu) || run<3>("f64 fma (1 dep chain)", 1, n_cu))
         return 1;
     return 0;
 }
