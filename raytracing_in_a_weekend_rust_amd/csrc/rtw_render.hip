@@ -172,7 +172,8 @@ struct KParams {
     uint16_t *spill_b;          // region B (cooperative groups)
     uint64_t spill_stride;      // levels per column (lane-major; RTW_SPILL_LEVEL_MAJOR builds:
                                 // columns per level)
-    uint64_t *stamps;           // RTW_STAMPS builds only: [wave][8]
+    uint64_t *stamps;           // RTW_STAMPS builds only: [wave][kStampRow], persistent kernel waves
+    uint64_t *stamps_drain;     // RTW_STAMPS builds only: [wave][kStampRow], rtw_park_leftover waves
     struct Parked *park;        // parked pixels (cursor lanes -> drain groups)
     uint32_t *park_count;       // parked pixels
     uint32_t *park_cursor;      // the drain groups' next queue ticket
@@ -2052,6 +2053,13 @@ __global__ __launch_bounds__(kBlock) void rtw_park_leftover(const KParams P) {
             atomicAdd(P.park_processed, 1u);
         }
     }
+#ifdef RTW_STAMPS
+    if ((threadIdx.x & 63u) == 0) {  // diagnostic: per drain wave, its section sums (tools/stamps_drain.py)
+        uint64_t *row = P.stamps_drain + (static_cast<uint64_t>(blockIdx.x) * (kBlock / 64u) + threadIdx.x / 64u) * kStampRow;
+        for (int k = 0; k < kStampSlots; ++k) row[k] = stp.acc[k];
+        row[14] = seg, row[15] = stamp_now();
+    }
+#endif
     tl.seg = seg;
     flush_tally(P, tl, false);
 }
@@ -2492,8 +2500,10 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     }
 #ifdef RTW_STAMPS
     {
-        // one row per wave of the persistent launch (one workgroup per CU)
-        const size_t nw = static_cast<size_t>(s->n_cu > 0 ? s->n_cu : 256) * (kPBlock / 64);
+        // one row per wave of the persistent launch (one workgroup per CU), then one
+        // per wave of the leftover launch (one kBlock workgroup per CU)
+        const size_t ncu = static_cast<size_t>(s->n_cu > 0 ? s->n_cu : 256);
+        const size_t np = ncu * (kPBlock / 64), nw = np + ncu * (kBlock / 64);
         static uint64_t *d_st = nullptr;
         static size_t cap = 0;
         if (nw * kStampRow * 8 > cap) {
@@ -2503,6 +2513,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         }
         HIPCHECK(hipMemset(d_st, 0, nw * kStampRow * 8));
         P.stamps = d_st;
+        P.stamps_drain = d_st + np * kStampRow;
         stamp_buf() = d_st;
         stamp_n() = nw;
     }
