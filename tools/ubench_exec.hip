@@ -59,6 +59,36 @@ __global__ __launch_bounds__(64) void bench(uint32_t active, uint64_t *cycles, d
                                    static_cast<double>(x0 ^ x1 ^ x2 ^ x3);
 }
 
+// Which SIMD each wave of a 768-thread workgroup lands on (HW_ID.SIMD_ID, bits 5:4),
+// with a large dynamic LDS request so one workgroup holds the CU (as the render does).
+__global__ __launch_bounds__(768) void simd_map(uint32_t *out) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t hw = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);  // hwreg(HW_REG_HW_ID, 4, 2)
+    if ((threadIdx.x & 63u) == 0) {
+        lds[threadIdx.x >> 6] = hw;
+        out[blockIdx.x * 12 + (threadIdx.x >> 6)] = hw & 3u;
+    }
+}
+
+int map_simds(int blocks) {
+    uint32_t *d;
+    CK(hipMalloc(&d, blocks * 12 * sizeof(uint32_t)));
+    hipLaunchKernelGGL(simd_map, dim3(blocks), dim3(768), 140 * 1024, nullptr, d);
+    CK(hipDeviceSynchronize());
+    std::vector<uint32_t> h(blocks * 12);
+    CK(hipMemcpy(h.data(), d, h.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    std::vector<int> same(12, 0);
+    for (int b = 0; b < blocks; ++b)
+        for (int w = 0; w < 12; ++w) same[w] += h[b * 12 + w] == h[w];
+    std::printf("wave -> SIMD in workgroup 0:");
+    for (int w = 0; w < 12; ++w) std::printf(" %u", h[w]);
+    std::printf("  (workgroups with the same map per wave:");
+    for (int w = 0; w < 12; ++w) std::printf(" %d", same[w]);
+    std::printf(" of %d)\n", blocks);
+    CK(hipFree(d));
+    return 0;
+}
+
 template <int kKind>
 int run(const char *name, int per_iter, int blocks) {
     uint64_t *cyc;
@@ -85,6 +115,7 @@ int run(const char *name, int per_iter, int blocks) {
 int main() {
     int n_cu = 0;
     CK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, 0));
+    if (map_simds(n_cu)) return 1;
     if (run<0>("f64 fma (8 chains)", 8, n_cu) || run<1>("f32 fma (8 chains)", 8, n_cu) ||
         run<2>("u32 shift-xor (4x2)", 8, n_cu) || run<3>("f64 fma (1 dep chain)", 1, n_cu))
         return 1;
