@@ -1275,6 +1275,13 @@ template <uint32_t kG>
 __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView &sv,
                                                const float4 *__restrict__ filt, uint32_t fsh, const Parked &q,
                                                uint64_t col, Tally &tl, Stamps &stp) {
+    if constexpr (kG == 64) {
+        // one group per wave: the spill column is wave-uniform -- in SGPRs, its offset
+        // col * stride is scalar arithmetic (held in a VGPR, the compiler spilled it to
+        // scratch and reloaded it at every drained segment behind a vmcnt(0) wait)
+        col = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(col >> 32))) << 32) |
+              static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(col)));
+    }
     const uint32_t sub = threadIdx.x & (kG - 1u);
     const uint32_t n = P.n_sph;
     const double4 *sph = sv.sph;
