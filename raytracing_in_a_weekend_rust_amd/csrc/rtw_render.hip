@@ -490,10 +490,10 @@ struct PixelLoc {
 __device__ __forceinline__ void lattice_off(const KParams &P, uint32_t k, double &offx, double &offy,
                                             double &offz) {
     const CamRef C(P);
-    if (P.s == 0) {
+    if (KP(s) == 0) {
         offx = C(C.kLatPos0 + 0), offy = C(C.kLatPos0 + 1), offz = C(C.kLatPos0 + 2);
     } else {
-        const uint32_t ly = P.s_magic ? __umulhi(k, P.s_magic) : k / P.s, lx = k - ly * P.s;
+        const uint32_t ly = KP(s_magic) ? __umulhi(k, KP(s_magic)) : k / KP(s), lx = k - ly * KP(s);
         const double fly = static_cast<double>(ly), flx = static_cast<double>(lx);
         offx = (C(C.kLatPos0 + 0) + C(C.kLatDy + 0) * fly) + C(C.kLatDx + 0) * flx;
         offy = (C(C.kLatPos0 + 1) + C(C.kLatDy + 1) * fly) + C(C.kLatDx + 1) * flx;
@@ -1666,8 +1666,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     acc[0] = acc[kThreads] = acc[2 * kThreads] = 0.;
                     pseg = 0;
                     spec = false;
-                    if (P.max_depth == 0) {  // every sample black, no Scene::hit call
-                        ps.k = P.n_off;
+                    if (KP(max_depth) == 0) {  // every sample black, no Scene::hit call
+                        ps.k = KP(n_off);
                         write_pixel(P, x, lr, ps);
                     } else if (P.prepark && order_map && KP(pcost)[pix] >= P.prepark) {
                         // a long serial chain by the probe's estimate: to a drain wave
@@ -1680,7 +1680,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         publish_parked(P, q);
                         ++tl.parked;
                     } else {
-                        gen_ray(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), 0, ps.rng, p, stp);
+                        gen_ray(P, PixelLoc(P, x, KP(row_begin) + lr * KP(row_step)), 0, ps.rng, p, stp);
                         need = false;
                     }
                 } else {
@@ -1761,7 +1761,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 rtw_num::div3(nx, ny, nz, r);  // (p - c) / r
                 const bool front = (p.dx * nx + p.dy * ny + p.dz * nz) < 0.;
                 if (!front) nx = -nx, ny = -ny, nz = -nz;
-                ended = p.depth + 1u >= P.max_depth;  // ray_color(depth >= max) -> black
+                ended = p.depth + 1u >= KP(max_depth);  // ray_color(depth >= max) -> black
                 double ndx = nx, ndy = ny, ndz = nz;
                 if (kind == RTW_METAL) {  // materials.rs:52-63: reflect(unit(dir), n) + fuzz u
                     const double dt = vx * nx + vy * ny + vz * nz;
@@ -1809,13 +1809,13 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
                     acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 }
-                done = ++ps.k >= P.n_off;
+                done = ++ps.k >= KP(n_off);
                 // park: the budget is spent, the rate runs away, or -- once the
                 // cursor is dry, so drain groups are about to be plentiful -- the
-                // estimated remaining work exceeds P.tail_segs
-                park = !done && (pseg >= P.seg_budget || (ps.k >= P.rate_k && pseg > P.rate_x * ps.k) ||
-                                 (endgame && P.n_off - ps.k >= kEndgameMinSamples) ||
-                                 (dry && static_cast<uint64_t>(P.n_off - ps.k) * pseg > static_cast<uint64_t>(P.tail_segs) * ps.k));
+                // estimated remaining work exceeds KP(tail_segs)
+                park = !done && (pseg >= KP(seg_budget) || (ps.k >= KP(rate_k) && pseg > KP(rate_x) * ps.k) ||
+                                 (endgame && KP(n_off) - ps.k >= kEndgameMinSamples) ||
+                                 (dry && static_cast<uint64_t>(KP(n_off) - ps.k) * pseg > static_cast<uint64_t>(KP(tail_segs)) * ps.k));
                 uint32_t *diag = KP(diag);
                 if ((done || park) && diag) {  // a pixel's records may come from two XCDs
                     atomicAdd(diag + 2 * pix, pseg);
@@ -1838,7 +1838,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             // phase 2 = the defocus disk (2 per try, accept len^2 < 1); each candidate is
             // judged in f32 first and rebuilt exactly only near the boundary
             const bool want_u = kind <= RTW_METAL;  // Lambertian or Metal
-            const bool want_disk = ended && !done && !park && !(P.defocus_angle <= 0.);
+            const bool want_disk = ended && !done && !park && !(KP(defocus_angle) <= 0.);
             // Speculation: a lane whose draws are done while others still loop goes on,
             // on a copy of its RNG state, with the unit vector its NEXT segment will
             // probably need (random_unit_vec's candidates do not depend on the
@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     need = true;
                 } else {  // the next sample's defocus disk point (camera.rs:452-456)
                     const double dpx = -1. + 2. * rtw_num::next01_of(dm0), dpy = -1. + 2. * rtw_num::next01_of(dm1);
-                    ray_from_disk(P, PixelLoc(P, x, P.row_begin + lr * P.row_step), ps.k, dpx, dpy, p);
+                    ray_from_disk(P, PixelLoc(P, x, KP(row_begin) + lr * KP(row_step)), ps.k, dpx, dpy, p);
                 }
             }
             STAMP(4);  // 4: fold + next sample / pixel end
