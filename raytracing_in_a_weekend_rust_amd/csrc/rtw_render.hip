@@ -767,6 +767,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         double lr, lg, lb;
         TrapHint th;
         bool done = shade<kTrap>(P, sv.sph, sv.shd, best, bt, a, p, ps.rng, spill, col, stride, lr, lg, lb, stp, &th);
+        STAMP(7);  // 7: scatter (after the hit record)
         if constexpr (kTrap) {
             // a total internal reflection keeps the path in the great circle it walks
             // (the chord, the normal and the reflection share S's centre), and the
@@ -775,14 +776,14 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
             // it is skipped (tir_no) until the path leaves the circle -- tracing on is
             // always exact, the forward only saves work
             const bool skip = th.tir && best == tir_no;
-            tir_no = -1;
+            if (!skip) tir_no = -1;  // kept through a run of TIR bounces in the same S
             if (!done && (th.lam || th.tir) && !skip) {
                 const uint32_t k = trap_forward(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
                 if (!k && th.tir) tir_no = best;
                 if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
             }
         }
-        STAMP(3);  // 3: hit record + scatter / sky
+        STAMP(3);  // 3: trapped-path check (kTrap)
         if (done) {
             // a depth-capped (or fast-forwarded) path's product is att x ... x 0 = +-0 with
             // finite attenuations, and adding +-0 to the sum changes no bit: no fold

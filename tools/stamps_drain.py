@@ -32,8 +32,8 @@ buf = np.zeros((nr.value, 16), dtype=np.uint64)
 assert f(buf.ctypes.data_as(C.POINTER(C.c_uint64)), nr.value, C.byref(nr)) == 0
 rows = buf[st.grid_blocks * 12:]  # after the persistent kernel's rows
 rows = rows[rows[:, 14] > 0]
-names = ["seg setup (Seg32)", "hit tail", "exact tests + min", "scatter+trap", "fold+next sample", "filter",
-         "hit record", "-", "lattice position", "defocus disk"]
+names = ["seg setup (Seg32)", "hit tail", "exact tests + min", "trap check", "fold+next sample", "filter",
+         "hit record", "scatter", "lattice position", "defocus disk"]
 tot = rows[:, :10].sum(axis=0).astype(np.float64)
 segs = float(rows[:, 14].sum())
 print(f"shard {shard}: kernel {st.kernel_ms:.2f} ms, leftover pixels {st.leftover_pixels}, drain waves {len(rows)}, "
@@ -41,3 +41,10 @@ print(f"shard {shard}: kernel {st.kernel_ms:.2f} ms, leftover pixels {st.leftove
 for k, nme in enumerate(names):
     if tot[k]:
         print(f"  {nme:20s} {tot[k] / tot.sum() * 100:6.2f}%  {tot[k] / segs:7.0f} cyc/segment")
+# the waves that drained the longest chains (a wave drains one pixel at a time; the
+# heaviest pixels dominate their wave's rows)
+top = np.argsort(rows[:, 14])[::-1][:3]
+for w in top:
+    r = rows[w, :10].astype(np.float64)
+    print(f"wave of {int(rows[w, 14])} segments: {r.sum() / rows[w, 14]:.0f} cyc/segment: " +
+          ", ".join(f"{nme} {r[k] / rows[w, 14]:.0f}" for k, nme in enumerate(names) if r[k]))
