@@ -57,3 +57,18 @@ for thr in (4, 6, 8, 10, 15, 20, 30):
     m = seg > thr
     print(f"  pixels > {thr:2d} seg/sample: {int(m.sum()):6d}, parked {int((m & p).sum()):6d}, "
           f"done p50/max {np.nanpercentile(done[m], 50):.1f}/{np.nanmax(done[m]):.1f} ms")
+# throughput over the kernel: each pixel's segments spread evenly between its hand-out and
+# its completion, summed per 2 ms bin (how much of the launch the tail leaves idle)
+ok = ~np.isnan(done) & ~np.isnan(ho)
+segs_px = d[:, 0].astype(np.float64)
+t_end = np.nanmax(done)
+edges = np.arange(0.0, t_end + 2.0, 2.0)
+rate = np.zeros(len(edges) - 1)
+for a, b, s_ in zip(ho[ok], done[ok], segs_px[ok]):
+    b = max(b, a + 1e-3)
+    lo = np.clip(edges[:-1], a, b)
+    hi = np.clip(edges[1:], a, b)
+    rate += s_ * (hi - lo) / (b - a)
+peak = rate.max()
+print("segment rate per 2 ms bin (fraction of the peak bin): " +
+      " ".join(f"{e:.0f}:{r / peak:.2f}" for e, r in zip(edges[:-1], rate)))
