@@ -43,7 +43,6 @@ import glob
 import hashlib
 import json
 import os
-import re
 import shutil
 import signal
 import subprocess
@@ -130,14 +129,26 @@ def profiler_active():
     return "rocprof" in pre or any(k.startswith("ROCPROF") for k in os.environ)
 
 
+def kernel_short_name(name):
+    """The kernel's own identifier from a demangled rocprofv3 name: the last
+    '::'-separated name before its template arguments / parameter list, e.g.
+    'void rtw_fast::(anonymous namespace)::rtw_fast_render<true>(rtw_fast::FastParams)'
+    -> 'rtw_fast_render', '(anonymous namespace)::rtw_seed_pixels((anonymous
+    namespace)::KParams)' -> 'rtw_seed_pixels', '__amd_rocclr_copyBuffer' -> itself."""
+    n = name.replace("(anonymous namespace)", "").strip()
+    if n.startswith("void "):
+        n = n[5:]
+    cut = min([i for i in (n.find("<"), n.find("(")) if i >= 0], default=len(n))
+    return n[:cut].split("::")[-1].strip() or name
+
+
 def read_counters(d):
     """{kernel short name: {counter: per-dispatch mean}} from a rocprofv3 csv dir."""
     acc, disp = {}, {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                m = re.search(r"\b((?:rtw|probe)_\w+)", row["Kernel_Name"])
-                short = m.group(1) if m else row["Kernel_Name"]
+                short = kernel_short_name(row["Kernel_Name"])
                 c = row["Counter_Name"]
                 k = (short, c)
                 acc[k] = acc.get(k, 0.0) + float(row["Counter_Value"])
@@ -275,33 +286,40 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(cam, sph, ns, mt, nm, s, stride):
+def cpu_baseline(cam, sph, ns, mt, nm, s, stride, repeats=3):
     """Oracle (C restatement) on a row sample, ref-faithful scheduler: one job per
     pixel pulled by `threads` workers, dyn dispatch + Arc-refcount traffic as in
-    camera.rs:269-292 / sphere.rs:69."""
+    camera.rs:269-292 / sphere.rs:69. Timed `repeats` times (the host's cores are
+    shared, so single timings move by +-10 %): `value` is the median, `runs` every
+    timing and `spread` (max - min) / median."""
     from oracle import oracle_ctypes as orc  # test infrastructure: checker/baseline only
 
     # the reference's own pool size on this host (not a cap of ours)
     threads, how = available_parallelism()
     if os.environ.get("RTW_CPU_THREADS"):
         threads, how = int(os.environ["RTW_CPU_THREADS"]), "RTW_CPU_THREADS override"
-    if stride <= 0:  # ~4 rows per thread at the headline spp: ~15 s of CPU work
+    if stride <= 0:  # ~2 rows per thread at the headline spp: ~6-8 s of CPU work per run
         work = cam.img_width * (s * s if s else 1) / (1200 * 529)
-        stride = max(1, int(round(cam.img_height * work / (4 * threads))))
+        stride = max(1, int(round(cam.img_height * work / (2 * threads))))
     n_rows = len(range(0, cam.img_height, stride))
-    t0 = time.perf_counter()
-    orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows), nthreads=threads, scheduler=0)
-    dt = time.perf_counter() - t0
     samples = n_rows * cam.img_width * (s * s if s else 1)
+    runs = []
+    for _ in range(max(1, repeats)):
+        t0 = time.perf_counter()
+        orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows), nthreads=threads, scheduler=0)
+        runs.append(samples / (time.perf_counter() - t0) / 1e6)
+    med = sorted(runs)[len(runs) // 2]
     # SURVEY.md 8(d): also the "clean" scheduler (rows pulled by the workers, direct
     # calls, no per-pixel job/refcount overhead), on the same sampled rows
     t0 = time.perf_counter()
     orc.render(cam, sph, ns, mt, nm, s, SEED, rows=(0, stride, n_rows), nthreads=threads, scheduler=1)
     c_dt = time.perf_counter() - t0
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+    return {"value": med, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"rows 0::{stride} ({n_rows} rows x {cam.img_width} px x {s * s} spp, "
-                      f"{samples / 1e6:.1f} Msamples) of the same image, {dt:.1f} s, "
-                      f"ref-faithful per-pixel jobs, {os.cpu_count()} host cpus visible",
+                      f"{samples / 1e6:.1f} Msamples) of the same image, median of {len(runs)} runs "
+                      f"({samples / med / 1e6:.1f} s each), ref-faithful per-pixel jobs, "
+                      f"{os.cpu_count()} host cpus visible",
+            "runs": [round(v, 4) for v in runs], "spread": round((max(runs) - min(runs)) / med, 4),
             "threads_rule": how, "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
             "clean_scheduler": {"value": samples / c_dt / 1e6, "unit": "Msamples/s", "cores": threads,
                                 "sample": f"rows 0::{stride} ({n_rows} rows), {c_dt:.1f} s, row jobs, "
@@ -461,9 +479,14 @@ def group_main(a, torch, rtw, shard):
     out["config"]["parallelism"] = (
         f"one process, rtw_group of {a.gpus} entries on devices {devs}, row-cyclic, gather "
         f"{info['gather']} to device {devs[0]} + un-permute there"
+        + (f" (RCCL fallback: {info['note']})" if info["fallback"] != "none" else "")
         + ("; devices repeated; not a scaling point" if repeated else ""))
+    mains = [p.main_kernel_ms for p in per]
     out["group"] = {"devices": devs, "visible_devices": visible, "repeated": repeated,
-                    "gather": info["gather"],
+                    "gather": info["gather"], "fallback": info["fallback"], "fallback_reason": info["note"],
+                    "slowest_entry": max(range(len(mains)), key=mains.__getitem__),
+                    "slowest_main_kernel_ms": round(max(mains), 3),
+                    "main_kernel_ms_spread": round((max(mains) - min(mains)) / max(mains), 4) if max(mains) else 0.0,
                     "entry_kernel_ms": [round(p.kernel_ms, 3) for p in per],
                     "entry_main_kernel_ms": [round(p.main_kernel_ms, 3) for p in per],
                     "entry_pixels": [p.pixels for p in per],
@@ -576,11 +599,16 @@ def main():
         elif world == 1:
             if a.pmc:
                 res, why = pmc_live(a)
-                if res and "insts" in res:
-                    pm, pm_source = pmc_summary(res, MAIN_KERNEL[a.mode], rtw.build_id()), "live rocprofv3 --pmc passes of a one-frame child run (this bench)"
+                kern = MAIN_KERNEL[a.mode]
+                if res and "insts" in res and kern in res["insts"]:
+                    pm, pm_source = pmc_summary(res, kern, rtw.build_id()), "live rocprofv3 --pmc passes of a one-frame child run (this bench)"
                     if a.pmc_out:
                         with open(a.pmc_out, "w") as f:
                             json.dump({**pm, "workload": workload_name(a), "mode": a.mode}, f, indent=1)
+                elif res and "insts" in res:  # the passes ran but matched no counters to the kernel
+                    seen = sorted({k for p in res.values() for k in p})
+                    pm_source = (f"live PMC passes ran but held no counters for kernel {kern} "
+                                 f"(kernels seen: {', '.join(seen[:8])}): frac/traffic not measured")
                 else:
                     pm_source = f"live PMC failed ({why})"
             if pm is None and a.mode == "parity" and workload_name(a) == "complex_1200x675_s23_d50":

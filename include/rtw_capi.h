@@ -264,12 +264,22 @@ int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap);
  * un-permuted there into the caller's device buffer. The gather is one ncclGather
  * over xGMI (RCCL communicators from ncclCommInitAll) when the entries are
  * distinct GPUs, device-to-device copies otherwise (a repeated device, or
- * RTW_GROUP_COPY_GATHER). Renders are blocking: on return the image is complete
- * in out_rgb_device. Bit-identical to a one-device render. */
+ * RTW_GROUP_COPY_GATHER). If RCCL cannot be loaded or its communicators fail to
+ * come up, the group falls back to the copy gather (peer access over xGMI) and
+ * says why (rtw_group_info.fallback, rtw_group_note); only RTW_GROUP_RCCL_ALWAYS
+ * makes that an error. Renders are blocking: on return the image is complete in
+ * out_rgb_device. The root device's first write to out_rgb_device is ordered
+ * after the work already queued on that device's null stream. Every rtw_group_*
+ * call restores the caller's current HIP device. Bit-identical to a one-device
+ * render. */
 typedef struct rtw_group rtw_group;
 #define RTW_GROUP_COPY_GATHER 1u /* flags: never RCCL, gather by device copies          */
-#define RTW_GROUP_RCCL_ALWAYS 2u /* flags: RCCL gather even for a one-entry group (tests) */
+#define RTW_GROUP_RCCL_ALWAYS 2u /* flags: RCCL gather even for a one-entry group; no
+                                    fallback: an RCCL failure is an error (tests)      */
+#define RTW_GROUP_RCCL_TRY 4u    /* flags: RCCL gather for a one-entry group too, with
+                                    the fallback (tests of the fallback on one GPU)    */
 enum { RTW_GATHER_NONE = 0, RTW_GATHER_COPY = 1, RTW_GATHER_RCCL = 2 };
+enum { RTW_FALLBACK_NONE = 0, RTW_FALLBACK_NO_RCCL = 1, RTW_FALLBACK_COMM_INIT = 2 };
 typedef struct rtw_group_info {
     uint32_t n_entries;     /* entries that rendered rows in the last render (min(n, H)) */
     uint32_t gather;        /* RTW_GATHER_* the last render used                        */
@@ -278,7 +288,10 @@ typedef struct rtw_group_info {
     double root_gather_ms;  /* root stream, from its own tile rendered to the image
                                complete: waiting for the other entries + gather +
                                un-permute                                               */
-    uint32_t fast, _pad;    /* the last render was f32 fast mode                        */
+    uint32_t fast;          /* the last render was f32 fast mode                        */
+    uint32_t fallback;      /* RTW_FALLBACK_*: why the group gathers by copies although
+                               its entries are distinct GPUs (RCCL unloadable, or
+                               ncclCommInitAll failed); text in rtw_group_note       */
 } rtw_group_info;
 int rtw_group_create(const int *devices, uint32_t n_devices, uint32_t flags, rtw_group **out);
 int rtw_group_destroy(rtw_group *g);
@@ -295,6 +308,12 @@ int rtw_group_render_fast(rtw_group *g, const rtw_camera *cam, uint32_t samples_
  * (nullable). */
 int rtw_group_stats(rtw_group *g, rtw_stats *total, rtw_stats *per_entry, uint32_t cap,
                     rtw_group_info *info);
+/* Why the group fell back from RCCL to the copy gather ("" if it did not). Owned by
+ * the group, valid until rtw_group_destroy. */
+const char *rtw_group_note(rtw_group *g);
+/* 1 if RCCL (librccl.so.1 with ncclCommInitAll/ncclGather) can be loaded, else 0 with
+ * the reason in why[0..cap) (nullable). Needs no GPU. */
+int rtw_rccl_available(char *why, size_t cap);
 
 /* ---- device probes (tests) ---- */
 /* Device jump-ahead seeds (the kernel's own code path) for a pixel range. */

@@ -82,15 +82,17 @@ class Stats(C.Structure):
 class GroupInfo(C.Structure):
     _fields_ = [("n_entries", C.c_uint32), ("gather", C.c_uint32), ("wall_ms", C.c_double),
                 ("render_ms_max", C.c_double), ("root_gather_ms", C.c_double),
-                ("fast", C.c_uint32), ("_pad", C.c_uint32)]
+                ("fast", C.c_uint32), ("fallback", C.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if not k.startswith("_")}
 
 
 GATHER_NAMES = {0: "none", 1: "copy", 2: "rccl"}
+FALLBACK_NAMES = {0: "none", 1: "rccl_unloadable", 2: "comm_init_failed"}
 GROUP_COPY_GATHER = 1
 GROUP_RCCL_ALWAYS = 2
+GROUP_RCCL_TRY = 4
 
 RTW_OK = 0
 ERRORS = {-1: "RTW_E_ARG", -2: "RTW_E_EMPTY_IMAGE", -3: "RTW_E_FUZZ", -4: "RTW_E_MAT_INDEX",
@@ -137,6 +139,8 @@ SIGNATURES = {
     "rtw_group_render": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
     "rtw_group_render_fast": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
     "rtw_group_stats": (C.c_int, [C.c_void_p, _P(Stats), _P(Stats), C.c_uint32, _P(GroupInfo)]),
+    "rtw_group_note": (C.c_char_p, [C.c_void_p]),
+    "rtw_rccl_available": (C.c_int, [C.c_char_p, C.c_size_t]),
     "rtw_threaded_render_fast": (C.c_int, [_P(Camera), _P(Sphere), C.c_uint32, _P(Material),
                                            C.c_uint32, C.c_uint32, U128, _P(Shard),
                                            _P(C.c_float), _P(Stats)]),

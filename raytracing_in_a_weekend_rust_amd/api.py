@@ -359,18 +359,31 @@ class Session:
             pass
 
 
+def rccl_available():
+    """(True, "") if RCCL (librccl.so.1 with ncclGather) can be loaded, else (False,
+    why). Needs no GPU."""
+    buf = C.create_string_buffer(256)
+    ok = lib.rtw_rccl_available(buf, len(buf))
+    return bool(ok), buf.value.decode()
+
+
 class Group:
     """Device-resident multi-GPU renders (rtw_group_*): one session per device entry
     (None = every visible device; an index may repeat), rows dealt cyclically, the
     row tiles gathered on the root device (entry 0) by ncclGather over xGMI when the
-    entries are distinct GPUs (device copies otherwise) and un-permuted there into a
-    caller device buffer. Blocking renders."""
+    entries are distinct GPUs (device copies otherwise, or when RCCL cannot be loaded
+    or initialised: `stats()[2]["fallback"]` and `note()` say why) and un-permuted
+    there into a caller device buffer. Blocking renders. rccl_always: RCCL even for
+    one entry, an RCCL failure is an error; rccl_try: RCCL even for one entry, with
+    the fallback."""
 
-    def __init__(self, devices=None, copy_gather: bool = False, rccl_always: bool = False):
+    def __init__(self, devices=None, copy_gather: bool = False, rccl_always: bool = False,
+                 rccl_try: bool = False):
         self.h = C.c_void_p()
         devs = list(devices or [])
         arr = (C.c_int * max(1, len(devs)))(*devs)
-        flags = (capi.GROUP_COPY_GATHER if copy_gather else 0) | (capi.GROUP_RCCL_ALWAYS if rccl_always else 0)
+        flags = ((capi.GROUP_COPY_GATHER if copy_gather else 0) | (capi.GROUP_RCCL_ALWAYS if rccl_always else 0)
+                 | (capi.GROUP_RCCL_TRY if rccl_try else 0))
         check(lib.rtw_group_create(arr if devs else None, len(devs), flags, C.byref(self.h)))
 
     def set_scene(self, sph, n_sph, mats, n_mats):
@@ -395,7 +408,14 @@ class Group:
         check(lib.rtw_group_stats(self.h, C.byref(total), per, max(1, info.n_entries), C.byref(info)))
         d = info.as_dict()
         d["gather"] = capi.GATHER_NAMES.get(info.gather, info.gather)
+        d["fallback"] = capi.FALLBACK_NAMES.get(info.fallback, info.fallback)
+        d["note"] = self.note()
         return total, [per[i] for i in range(info.n_entries)], d
+
+    def note(self) -> str:
+        """Why the group gathers by device copies although its entries are distinct
+        GPUs ("" when it does not)."""
+        return (lib.rtw_group_note(self.h) or b"").decode()
 
     def close(self):
         if self.h:

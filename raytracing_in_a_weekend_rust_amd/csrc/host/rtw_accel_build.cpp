@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "rtw_accel.h"
+#include "rtw_internal.h"
 
 namespace rtw_accel {
 namespace {
@@ -231,7 +232,7 @@ bool build(const double *centers, const double *radii, const float *r2p, uint32_
     }
     if (m == 0) return true;
     Builder b{centers, radii, r2p, rest, &out};
-    b.median = std::getenv("RTW_BVH_MEDIAN") != nullptr;
+    b.median = rtw::Knobs().get("RTW_BVH_MEDIAN") != nullptr;  // A/B only (RTW_AB)
     b.wide(0, m, 1);
     out.n_node = static_cast<uint32_t>(out.nodes.size() / kNodeFloats);
     return true;

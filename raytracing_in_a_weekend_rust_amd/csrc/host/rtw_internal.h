@@ -3,6 +3,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -32,5 +33,20 @@ inline void add_stats(rtw_stats &a, const rtw_stats &b, bool first) {
 struct Error : std::runtime_error {
     int code;
     Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+// Scheduling, strategy and diagnostic switches (RTW_ACCEL, RTW_HEAVY, RTW_DIAG, ...)
+// are read from the environment only when RTW_AB is set to a non-zero value: A/B
+// runs, the developer tools and the strategy tests. A production render reads
+// RTW_AB once and nothing else, so its schedule cannot change with the caller's
+// environment (the reference's Camera::threaded_render takes no tuning either,
+// camera.rs:223-227). Results are identical either way; only the schedule moves.
+struct Knobs {
+    bool on;
+    Knobs() {
+        const char *e = std::getenv("RTW_AB");
+        on = e && *e && !(e[0] == '0' && e[1] == '\0');
+    }
+    const char *get(const char *name) const { return on ? std::getenv(name) : nullptr; }
 };
 }  // namespace rtw

@@ -50,6 +50,6 @@ constexpr uint32_t stack_slots(uint32_t depth) { return 3 * depth + 2; }
 size_t lds_bytes(uint32_t n_sph, uint32_t n_node, uint32_t n_stack, bool *scene_in_lds);
 
 // Enqueues the render (zeroes the cursor and counters first).
-hipError_t launch(const FastParams &P, int n_cu, hipStream_t st);
+hipError_t launch(const FastParams &P, int n_cu, hipStream_t st, bool scene_lds = true);
 
 }  // namespace rtw_fast

@@ -419,7 +419,7 @@ size_t lds_bytes(uint32_t n_sph, uint32_t n_node, uint32_t n_stack, bool *scene_
     return *scene_in_lds ? stacks + scene : (stacks ? stacks : 16);
 }
 
-hipError_t launch(const FastParams &P, int n_cu, hipStream_t st) {
+hipError_t launch(const FastParams &P, int n_cu, hipStream_t st, bool scene_lds) {
     hipError_t e = hipMemsetAsync(P.cursor, 0, sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(P.counters, 0, 5 * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
@@ -429,7 +429,7 @@ hipError_t launch(const FastParams &P, int n_cu, hipStream_t st) {
         static_cast<uint64_t>(n_cu > 0 ? n_cu : 256) * 2, (npix + kWaves - 1) / kWaves));
     bool in_lds = false;
     size_t lds = lds_bytes(P.n_sph, P.n_node, P.n_stack, &in_lds);
-    if (const char *e = std::getenv("RTW_FAST_LDS"); e && !std::atoi(e) && in_lds) {  // A/B knob
+    if (!scene_lds && in_lds) {  // A/B: RTW_FAST_LDS=0 under RTW_AB (the scene read from HBM)
         in_lds = false;
         lds = P.n_stack ? static_cast<size_t>(P.n_stack) * kBlock * sizeof(uint16_t) : 16;
     }

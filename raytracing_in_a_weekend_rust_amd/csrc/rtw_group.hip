@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -60,30 +61,60 @@ struct Rccl {
     const char *(*error_string)(ncclResult_t) = nullptr;
 };
 
-Rccl &rccl() {
+// RCCL, opened on first use. The soname list can be replaced under RTW_AB
+// (RTW_RCCL_SONAME, ':'-separated) so tests can make RCCL unloadable.
+Rccl &rccl_handle(std::string *why) {
     static Rccl r;
+    static std::string err;
     static std::once_flag once;
     std::call_once(once, [] {
-        for (const char *name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            if ((r.so = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+        std::vector<std::string> names = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+        if (const char *e = rtw::Knobs().get("RTW_RCCL_SONAME")) {
+            names.clear();
+            std::string v(e);
+            for (size_t a = 0; a <= v.size();) {
+                const size_t b = std::min(v.find(':', a), v.size());
+                if (b > a) names.push_back(v.substr(a, b - a));
+                a = b + 1;
+            }
         }
-        if (!r.so) return;
+        for (const auto &name : names) {
+            if ((r.so = dlopen(name.c_str(), RTLD_NOW | RTLD_GLOBAL))) break;
+        }
+        if (!r.so) {
+            std::string tried;
+            for (const auto &name : names) tried += (tried.empty() ? "" : ", ") + name;
+            err = "RCCL not loadable (dlopen of " + tried + " failed)";
+            return;
+        }
         r.comm_init_all = reinterpret_cast<decltype(r.comm_init_all)>(dlsym(r.so, "ncclCommInitAll"));
         r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(r.so, "ncclCommDestroy"));
         r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(r.so, "ncclGather"));
         r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(r.so, "ncclGroupStart"));
         r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(r.so, "ncclGroupEnd"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(r.so, "ncclGetErrorString"));
+        if (!r.comm_init_all || !r.comm_destroy || !r.gather || !r.group_start || !r.group_end) {
+            err = "RCCL loaded but lacks ncclCommInitAll/ncclGather/ncclGroupStart/End";
+            r.so = nullptr;
+        }
     });
-    if (!r.so || !r.comm_init_all || !r.comm_destroy || !r.gather || !r.group_start || !r.group_end)
-        throw rtw::Error(RTW_E_HIP, "RCCL (librccl.so.1 with ncclGather) not loadable");
+    if (why) *why = err;
+    return r;
+}
+
+bool rccl_ok(std::string *why) { return rccl_handle(why).so != nullptr; }
+
+Rccl &rccl() {
+    std::string why;
+    Rccl &r = rccl_handle(&why);
+    if (!r.so) throw rtw::Error(RTW_E_HIP, why);
     return r;
 }
 
 void nccl_check(ncclResult_t rc, const char *what) {
     if (rc != ncclSuccess) {
-        const char *msg = rccl().error_string ? rccl().error_string(rc) : "";
-        throw rtw::Error(RTW_E_HIP, std::string(what) + ": " + msg);
+        const Rccl &r = rccl_handle(nullptr);
+        throw rtw::Error(RTW_E_HIP, std::string(what) + ": " + (r.error_string ? r.error_string(rc) : ""));
     }
 }
 
@@ -111,10 +142,13 @@ struct Entry {
 struct rtw_group {
     std::vector<Entry> e;
     uint32_t gather = RTW_GATHER_NONE;  // for n > 1 entries
-    bool force_rccl = false;            // RTW_GROUP_RCCL_ALWAYS: RCCL even for one entry
+    bool force_rccl = false;            // RTW_GROUP_RCCL_ALWAYS: RCCL even for one entry (strict)
+    bool single_rccl = false;           // a one-entry group gathers through RCCL (ALWAYS, or TRY that worked)
+    std::string note;                   // why the group fell back from RCCL to device copies ("" = it did not)
     void *gathered = nullptr;           // root: n x tile, tile i at slot i
     size_t gathered_cap = 0;
     hipEvent_t g0 = nullptr, g1 = nullptr;  // root stream: root tile ready -> image complete
+    hipEvent_t caller = nullptr;            // root device's null stream at the call (ordering)
     rtw_group_info info{};
     std::mutex mu;
 };
@@ -134,7 +168,7 @@ void destroy(rtw_group *g) {
     for (auto &x : g->e) {
         (void)hipSetDevice(x.device);
         if (x.stream) (void)hipStreamSynchronize(x.stream);
-        if (x.comm) (void)rccl().comm_destroy(x.comm);
+        if (x.comm) (void)rccl_handle(nullptr).comm_destroy(x.comm);
         if (x.tile) (void)hipFree(x.tile);
         if (x.ev0) (void)hipEventDestroy(x.ev0);
         if (x.ev1) (void)hipEventDestroy(x.ev1);
@@ -145,6 +179,7 @@ void destroy(rtw_group *g) {
     if (g->gathered) (void)hipFree(g->gathered);
     if (g->g0) (void)hipEventDestroy(g->g0);
     if (g->g1) (void)hipEventDestroy(g->g1);
+    if (g->caller) (void)hipEventDestroy(g->caller);
     delete g;
 }
 
@@ -173,21 +208,44 @@ void create(const int *devices, uint32_t n_devices, uint32_t flags, rtw_group **
         hip_check(hipSetDevice(devs[0]), "hipSetDevice");
         hip_check(hipEventCreate(&g->g0), "hipEventCreate");
         hip_check(hipEventCreate(&g->g1), "hipEventCreate");
+        hip_check(hipEventCreateWithFlags(&g->caller, hipEventDisableTiming), "hipEventCreate");
         std::vector<int> sorted = devs;
         std::sort(sorted.begin(), sorted.end());
         const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
         g->force_rccl = (flags & RTW_GROUP_RCCL_ALWAYS) != 0;
         if (g->force_rccl && (!distinct || (flags & RTW_GROUP_COPY_GATHER)))
             throw rtw::Error(RTW_E_ARG, "RTW_GROUP_RCCL_ALWAYS needs distinct devices and no RTW_GROUP_COPY_GATHER");
-        if (devs.size() > 1 || g->force_rccl) {
+        const bool try_single = (flags & RTW_GROUP_RCCL_TRY) != 0 && !(flags & RTW_GROUP_COPY_GATHER);
+        if (devs.size() > 1 || g->force_rccl || try_single) {
             g->gather = (distinct && !(flags & RTW_GROUP_COPY_GATHER)) ? RTW_GATHER_RCCL : RTW_GATHER_COPY;
             if (g->gather == RTW_GATHER_RCCL) {
-                std::vector<ncclComm_t> comms(devs.size());
-                nccl_check(rccl().comm_init_all(comms.data(), static_cast<int>(devs.size()), devs.data()),
-                           "ncclCommInitAll");
-                for (size_t i = 0; i < devs.size(); ++i) g->e[i].comm = comms[i];
-            } else {
+                // RCCL when it loads and its communicators come up; otherwise the
+                // device-copy gather (same slots, same image), with the reason kept in
+                // rtw_group_note -- unless the caller asked for RCCL strictly
+                std::string why;
+                if (rccl_ok(&why)) {
+                    std::vector<ncclComm_t> comms(devs.size());
+                    const ncclResult_t rc =
+                        rccl().comm_init_all(comms.data(), static_cast<int>(devs.size()), devs.data());
+                    if (rc == ncclSuccess) {
+                        for (size_t i = 0; i < devs.size(); ++i) g->e[i].comm = comms[i];
+                    } else {
+                        const char *m = rccl().error_string ? rccl().error_string(rc) : "";
+                        why = std::string("ncclCommInitAll failed: ") + m;
+                        g->info.fallback = RTW_FALLBACK_COMM_INIT;
+                    }
+                } else {
+                    g->info.fallback = RTW_FALLBACK_NO_RCCL;
+                }
+                if (g->info.fallback != RTW_FALLBACK_NONE) {
+                    if (g->force_rccl) throw rtw::Error(RTW_E_HIP, why);
+                    g->note = why;
+                    g->gather = RTW_GATHER_COPY;
+                }
+            }
+            if (g->gather == RTW_GATHER_COPY) {
                 // copies from other devices' tiles: peer access where the pair allows it
+                hip_check(hipSetDevice(devs[0]), "hipSetDevice");
                 for (size_t i = 1; i < devs.size(); ++i) {
                     int ok = 0;
                     if (devs[i] != devs[0] && hipDeviceCanAccessPeer(&ok, devs[0], devs[i]) == hipSuccess && ok) {
@@ -198,6 +256,8 @@ void create(const int *devices, uint32_t n_devices, uint32_t flags, rtw_group **
                     }
                 }
             }
+            g->single_rccl = devs.size() == 1 && g->gather == RTW_GATHER_RCCL;
+            if (devs.size() == 1 && g->gather == RTW_GATHER_COPY) g->gather = RTW_GATHER_NONE;  // TRY fell back
         }
         g->info.n_entries = static_cast<uint32_t>(devs.size());
         g->info.gather = g->gather;
@@ -220,10 +280,17 @@ void render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128
     const size_t row_elems = static_cast<size_t>(W) * 3, row_bytes = row_elems * sizeof(T);
     const size_t tile_bytes = tile_rows * row_bytes;
     const bool all_entries = n == g->e.size();
-    const bool use_rccl = all_entries && g->gather == RTW_GATHER_RCCL && (n > 1 || g->force_rccl);
+    const bool use_rccl = all_entries && g->gather == RTW_GATHER_RCCL && (n > 1 || g->single_rccl);
     const uint32_t gather = use_rccl ? RTW_GATHER_RCCL : n == 1 ? RTW_GATHER_NONE : RTW_GATHER_COPY;
     Entry &root = g->e[0];
     if (gather != RTW_GATHER_NONE) grow(g->gathered, g->gathered_cap, n * tile_bytes, root.device);
+    // The root stream is non-blocking, so order it after the work the caller already
+    // queued on the root device's null stream (torch's default stream), which may
+    // still read or write `out`: the root stream's first write to `out` (the one-entry
+    // render, or the un-permute) waits for it.
+    hip_check(hipSetDevice(root.device), "hipSetDevice");
+    hip_check(hipEventRecord(g->caller, nullptr), "hipEventRecord (caller stream)");
+    hip_check(hipStreamWaitEvent(root.stream, g->caller, 0), "hipStreamWaitEvent");
 
     // 1. every entry's rows, enqueued on its own stream (asynchronous)
     for (uint32_t i = 0; i < n; ++i) {
@@ -300,7 +367,20 @@ void render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128
 
 }  // namespace
 
+// The caller's current device is restored on every exit of an rtw_group_* call
+// (the calls switch devices per entry; a torch caller's allocations must not move).
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
 #define RTW_GROUP_GUARD(body)                 \
+    DeviceGuard device_guard_;                \
     try {                                     \
         body;                                 \
         return RTW_OK;                        \
@@ -320,8 +400,22 @@ int rtw_group_create(const int *devices, uint32_t n_devices, uint32_t flags, rtw
 }
 
 int rtw_group_destroy(rtw_group *g) {
+    DeviceGuard guard;
     if (g) destroy(g);
     return RTW_OK;
+}
+
+const char *rtw_group_note(rtw_group *g) { return g ? g->note.c_str() : ""; }
+
+int rtw_rccl_available(char *why, size_t cap) {
+    std::string w;
+    const bool ok = rccl_ok(&w);
+    if (why && cap) {
+        const size_t k = std::min(cap - 1, w.size());
+        std::memcpy(why, w.data(), k);
+        why[k] = '\0';
+    }
+    return ok ? 1 : 0;
 }
 
 int rtw_group_set_scene(rtw_group *g, const rtw_sphere *spheres, uint32_t n_spheres, const rtw_material *mats,

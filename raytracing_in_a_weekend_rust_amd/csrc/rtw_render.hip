@@ -2385,6 +2385,7 @@ void order_after_last(rtw_session *s, hipStream_t st) {
 void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
             const rtw_shard *shard_in, double *out, hipStream_t stream) {
     if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
+    const rtw::Knobs kn;  // tuning only under RTW_AB (rtw_internal.h)
     if (!s->scene_set) throw rtw::Error(RTW_E_ARG, "session has no scene");
     if (cam->img_height == 0 || cam->img_width == 0)
         throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");  // camera.rs:267
@@ -2432,7 +2433,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.leaves = s->d_leaves;
     P.always = s->d_always;
     P.jump_bits = bits;
-    P.att_finite = (s->att_finite && !std::getenv("RTW_FOLD_BLACK")) ? 1u : 0u;
+    P.att_finite = (s->att_finite && !kn.get("RTW_FOLD_BLACK")) ? 1u : 0u;
     P.seed_lo = seed.lo;
     P.seed_hi = seed.hi;
     P.sph = s->d_sph;
@@ -2494,7 +2495,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     {
         // idle-wait guard (SpinGuard): RTW_SPIN_GUARD_MS of no progress anywhere
         double ms = 100.;
-        if (const char *e = std::getenv("RTW_SPIN_GUARD_MS")) ms = std::atof(e);
+        if (const char *e = kn.get("RTW_SPIN_GUARD_MS")) ms = std::atof(e);
         P.spin_guard = static_cast<uint64_t>(std::max(0., ms) * 1e5);  // 100 MHz ticks
     }
     P.park_flag = s->d_park_flag;
@@ -2502,7 +2503,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     {
         // budget = X x samples per pixel (X: RTW_BUDGET_X, default kBudgetX; 0 = off)
         double bx = kBudgetX;
-        if (const char *e = std::getenv("RTW_BUDGET_X")) bx = std::atof(e);
+        if (const char *e = kn.get("RTW_BUDGET_X")) bx = std::atof(e);
         const double b = bx * static_cast<double>(P.n_off);
         P.seg_budget = (bx > 0. && b < 4e9) ? static_cast<uint32_t>(std::ceil(b)) : 0xffffffffu;
     }
@@ -2529,7 +2530,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.counters = s->d_counters;
     P.diag = nullptr;
     P.diag_ev = 0;
-    if (const char *e = std::getenv("RTW_DIAG")) {
+    if (const char *e = kn.get("RTW_DIAG")) {
         if (std::atoi(e) != 0) {
             // RTW_DIAG=2: also per pixel {hand-out, first park, first drain claim} clocks
             // after the {segments, completion} records
@@ -2554,9 +2555,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     hipStream_t st = stream;  // NULL = HIP's null stream (torch's default stream handle is 0)
     order_after_last(s, st);
     // Scene::hit strategy: RTW_ACCEL=0 f64 scan, 1 filtered scan, 2 BVH (default
-    // when the scene is eligible); A/B and tests only -- results are identical.
+    // when the scene is eligible); A/B and tests only (RTW_AB) -- results are identical.
     int mode = s->has_bvh ? kBvh : kScanF32;
-    if (const char *e = std::getenv("RTW_ACCEL")) mode = std::atoi(e);
+    if (const char *e = kn.get("RTW_ACCEL")) mode = std::atoi(e);
     if (mode == kBvh && !s->has_bvh) mode = kScanF32;
     if (mode < kScanF64 || mode > kBvh) mode = kScanF32;
     size_t lds = lds_bytes_for(P.n_sph, P.n_node, P.n_leaf, mode == kBvh, P.n_nbr);
@@ -2568,7 +2569,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 8 * sizeof(uint32_t), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     P.order = 2;
-    if (const char *e = std::getenv("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
+    if (const char *e = kn.get("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
     uint32_t grid_p = 0;
     if (P.n_rows) {
         const uint64_t npix = static_cast<uint64_t>(P.n_rows) * P.W;
@@ -2590,7 +2591,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
             P.probe_sub = 1;
-            if (const char *e = std::getenv("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+            if (const char *e = kn.get("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
             if (P.probe_sub > 1) HIPCHECK(hipMemsetAsync(s->d_pcost, 0, npix * sizeof(uint32_t), st));
             // probe: scene + per-lane walk stacks in LDS when they fit, one workgroup per CU
             KParams Q = P;
@@ -2609,7 +2610,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         }
         const int pblock = kPBlock;
         int coop_g = 64;  // lanes per parked pixel in the persistent drain (RTW_COOPG=16: 4 per wave)
-        if (const char *e = std::getenv("RTW_COOPG")) coop_g = std::atoi(e) == 16 ? 16 : 64;
+        if (const char *e = kn.get("RTW_COOPG")) coop_g = std::atoi(e) == 16 ? 16 : 64;
         // LDS: the scene view + pass-1 records when they fit beside the per-lane areas
         const size_t lane_b = lane_lds_bytes(kPBlock);
         bool lds_scene = use_lds && lds + lane_b <= kLdsCap;
@@ -2654,7 +2655,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // rank 23.0 -> 17.9 ms at s=10 with the rate rule's earlier start below)
         uint32_t heavy = fill >= 0.75 && small_fill ? (P.n_off >= 400u ? kHeavyPerBlockFull : kHeavyPerBlockFullShort)
                                                     : kHeavyPerBlock;
-        if (const char *e = std::getenv("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_HEAVY")) heavy = static_cast<uint32_t>(std::atoi(e));
         if (heavy >= wpb) heavy = wpb - 1;
         P.heavy_per_block = heavy;
         // priority waves join the cursor once it has handed out kJoinPct % of the
@@ -2666,7 +2667,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // (N=2 rank: 93 -> 111 ms, N=4: 79 -> 103 ms with the join).
         const uint64_t cursor_lanes = static_cast<uint64_t>(grid_p) * (wpb - heavy) * 64u;
         double join_pct = npix >= 4u * cursor_lanes ? kJoinPct : 0.;
-        if (const char *e = std::getenv("RTW_JOIN")) join_pct = std::atof(e);
+        if (const char *e = kn.get("RTW_JOIN")) join_pct = std::atof(e);
         P.join_at = join_pct > 0. ? static_cast<uint32_t>(std::min(npix, static_cast<uint64_t>(
                                         join_pct / 100. * static_cast<double>(npix))))
                                   : 0xffffffffu;
@@ -2691,21 +2692,21 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // RTW_ENDGAME: the remaining-pixel threshold, 0 = off.
         const bool small_for_endgame = npix < 2u * static_cast<uint64_t>(grid_p) * pblock;
         P.endgame = small_for_endgame ? grid_p * wpb * (64u / static_cast<uint32_t>(coop_g)) : 0u;
-        if (const char *e = std::getenv("RTW_ENDGAME")) P.endgame = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_ENDGAME")) P.endgame = static_cast<uint32_t>(std::atoi(e));
         P.tail_segs = small_shard ? 0xffffffffu
                                   : static_cast<uint32_t>(std::max(64., std::round(kTailSegsPerSample * P.n_off)));
-        if (const char *e = std::getenv("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
-        if (const char *e = std::getenv("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
-        if (const char *e = std::getenv("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
-        if (const char *e = std::getenv("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
+        if (const char *e = kn.get("RTW_TAIL")) P.tail_segs = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_RATE_X")) P.rate_x = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_RATE_K")) P.rate_k = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_DRAIN_OFF")) P.drain_off = std::atoi(e) != 0 ? 1u : 0u;
         // priority waves drain at raised issue priority only in small shards, where the
         // drained chains set the end; in a full image they have the time and their
         // issue-bound segments would take slots from the cursor waves (N=1 123.6 ->
         // 122.2 ms with 0; N=4 rank 60.0 -> 63.1 ms with 0: ab_heavy_prio.log)
         P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
-        if (const char *e = std::getenv("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
-        if (const char *e = std::getenv("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
-        if (const char *e = std::getenv("RTW_DRAIN_PRIO")) P.drain_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
+        if (const char *e = kn.get("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
+        if (const char *e = kn.get("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
+        if (const char *e = kn.get("RTW_DRAIN_PRIO")) P.drain_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
         void *args[] = {&P};
@@ -2794,7 +2795,9 @@ void render_fast(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, r
     order_after_last(s, st);
     HIPCHECK(hipEventRecord(s->ev0, st));
     HIPCHECK(hipEventRecord(s->ev_k0, st));
-    HIPCHECK(rtw_fast::launch(F, s->n_cu, st));
+    const rtw::Knobs kn;  // tuning only under RTW_AB (rtw_internal.h)
+    const char *lds_knob = kn.get("RTW_FAST_LDS");
+    HIPCHECK(rtw_fast::launch(F, s->n_cu, st, !(lds_knob && !std::atoi(lds_knob))));
     HIPCHECK(hipEventRecord(s->ev_k1, st));
     hipLaunchKernelGGL(rtw_latch_check<unsigned long long>, dim3(1), dim3(64), 0, st,
                        static_cast<const unsigned long long *>(s->d_fcount + 2),

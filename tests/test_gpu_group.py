@@ -119,3 +119,97 @@ def test_camera_threaded_render_uses_every_device(tmp_path):
     ref, seg = orc.render(cam.raw, sph, n, mt, nm, 1, SEED)
     assert np.array_equal(fb, ref) and st.segments == seg
     assert ppm.read_bytes() == orc.format_ppm(ref)
+
+
+def test_group_orders_after_callers_null_stream():
+    """The group's streams are non-blocking; its first write to `out` must still come
+    after work the caller queued on the device's null stream (torch's default
+    stream). A long spin then a fill of `out` precede the render: the render's
+    image must be what is left."""
+    cam, sph, n, mt, nm = scene()
+    ref, _ = orc.render(cam.raw, sph, n, mt, nm, 2, SEED)
+    assert torch.cuda.current_stream().cuda_stream == 0  # the null stream
+    for devices in ([0], [0, 0]):
+        g = rtw.Group(devices)
+        g.set_scene(sph, n, mt, nm)
+        out = torch.zeros((27, 48, 3), dtype=torch.float64, device="cuda:0")
+        torch.cuda._sleep(200_000_000)  # ~0.1 s of spinning on the null stream
+        out.fill_(-7.0)
+        g.render(cam.raw, 2, SEED, out.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref), devices
+        g.close()
+
+
+_FALLBACK_CHILD = r"""
+import sys, numpy as np, torch
+import raytracing_in_a_weekend_rust_amd as rtw
+SEED = rtw.DEFAULT_SEED
+cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 27, 48, 20)
+ref, st = rtw.render_flat(cam.raw, sph, n, mt, nm, 2, SEED)
+ok, why = rtw.rccl_available()
+assert not ok and "not loadable" in why, why
+g = rtw.Group([0], rccl_try=True)
+g.set_scene(sph, n, mt, nm)
+out = torch.full((27, 48, 3), -1.0, dtype=torch.float64, device="cuda:0")
+g.render(cam.raw, 2, SEED, out.data_ptr())
+total, per, info = g.stats()
+assert info["fallback"] == "rccl_unloadable" and info["gather"] == "none", info
+assert "not loadable" in info["note"], info
+assert np.array_equal(out.cpu().numpy(), ref) and total.segments == st.segments
+g.close()
+try:
+    rtw.Group([0], rccl_always=True)
+except rtw.RtwError as e:
+    assert "not loadable" in str(e), e
+else:
+    raise AssertionError("rccl_always must fail without RCCL")
+print("fallback ok")
+"""
+
+
+def test_group_falls_back_when_rccl_is_unloadable():
+    """RCCL made unloadable (RTW_RCCL_SONAME under RTW_AB, in a child process: the
+    library opens RCCL once per process): a group that would gather through RCCL
+    falls back, says why, and renders the same image; RTW_GROUP_RCCL_ALWAYS fails
+    loudly instead."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, RTW_AB="1", RTW_RCCL_SONAME="librccl_missing_for_test.so")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _FALLBACK_CHILD], cwd=root, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0 and "fallback ok" in out.stdout, out.stdout + out.stderr
+
+
+def test_group_rccl_try_uses_rccl_when_present():
+    cam, sph, n, mt, nm = scene()
+    ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, SEED)
+    fb, total, _, info = group_render([0], cam.raw, sph, n, mt, nm, 2, rccl_try=True)
+    assert info["gather"] == "rccl" and info["fallback"] == "none" and info["note"] == ""
+    assert np.array_equal(fb, ref) and total.segments == seg
+
+
+two_gpus = pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs")
+
+
+@two_gpus
+@pytest.mark.parametrize("devices,kw,gather", [([0, 1], {}, "rccl"), ([0, 1], {"copy_gather": True}, "copy"),
+                                               ([1, 0], {}, "rccl")])
+def test_group_distinct_gpus(devices, kw, gather):
+    """Distinct GPUs: the ncclGather over xGMI and the peer-copy gather, and a root
+    that is not device 0 (the image lands on devices[0]); the caller's current
+    device is restored."""
+    cam, sph, n, mt, nm = scene()
+    ref, seg = orc.render(cam.raw, sph, n, mt, nm, 2, SEED)
+    torch.cuda.set_device(0)
+    g = rtw.Group(devices, **kw)
+    g.set_scene(sph, n, mt, nm)
+    out = torch.full((27, 48, 3), -1.0, dtype=torch.float64, device=f"cuda:{devices[0]}")
+    g.render(cam.raw, 2, SEED, out.data_ptr())
+    assert torch.cuda.current_device() == 0
+    total, per, info = g.stats()
+    g.close()
+    assert info["gather"] in (gather, "copy") and (info["gather"] == gather or info["fallback"] != "none")
+    assert np.array_equal(out.cpu().numpy(), ref) and total.segments == seg

@@ -16,6 +16,14 @@ from tests.golden_io import fb_of, load, renders
 
 pytestmark = pytest.mark.gpu
 SEED = rtw.DEFAULT_SEED
+
+
+@pytest.fixture(autouse=True)
+def _ab_switch(monkeypatch):
+    """The strategy / schedule knobs these tests set (RTW_ACCEL, RTW_BUDGET_X, ...)
+    are read by the library only under RTW_AB=1 (rtw_internal.h Knobs); with no knob
+    set the A/B path is the production path."""
+    monkeypatch.setenv("RTW_AB", "1")
 P = C.POINTER(C.c_double)
 
 
@@ -242,6 +250,21 @@ def test_strategies_bit_exact(monkeypatch, accel, budget, coop):
         assert st.parked_pixels > 45 * 80 // 2
     if accel == "2" and budget == "0":
         assert st.node_visits > 0 and st.brute_segments < st.segments // 100
+
+
+def test_knobs_ignored_without_ab_switch(monkeypatch):
+    """Production renders take no tuning from the environment: without RTW_AB the
+    strategy knobs are not read (the BVH stays on, nothing is parked)."""
+    monkeypatch.delenv("RTW_AB")
+    monkeypatch.setenv("RTW_ACCEL", "0")
+    monkeypatch.setenv("RTW_BUDGET_X", "0.01")
+    cam, sph, n, mt, nm = rtw.builtin_scene("complex", SEED, 45, 80, 50)
+    fb, st = gpu(cam, sph, n, mt, nm, 3, SEED)
+    assert st.accel == 2 and st.parked_pixels < 45 * 80
+    monkeypatch.setenv("RTW_AB", "1")
+    fb2, st2 = gpu(cam, sph, n, mt, nm, 3, SEED)
+    assert st2.accel == 0 and st2.parked_pixels == 45 * 80
+    assert np.array_equal(fb, fb2) and st.segments == st2.segments
 
 
 @pytest.mark.parametrize("accel,budget,coop", [("2", "0.01", "16"), ("2", "0.7", "64")])

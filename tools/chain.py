@@ -3,6 +3,7 @@ row 455 of the bench image (shard (455, 675, 1)), so the heavy pixels' chains ru
 nearly alone on the GPU, and prints the kernel time, the heaviest pixels and the
 implied time per segment, per strategy knob set given as argv (K=V,...)."""
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import numpy as np

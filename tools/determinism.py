@@ -1,6 +1,7 @@
 """Developer tool: renders the final scene twice per configuration and reports
 differing pixels (nondeterminism hunt) plus the park count."""
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import numpy as np

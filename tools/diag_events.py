@@ -3,6 +3,7 @@ first park, first drain claim and completion of the heaviest pixels and of the
 last finishers, and the park -> claim waits of every parked pixel.
 usage: python tools/diag_events.py [S] [N r]   (shard r of an N-row-cyclic split)"""
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import numpy as np

@@ -1,6 +1,7 @@
 """Developer tool: per-pixel segment counts and completion times of the bench
 workload (RTW_DIAG=1): cost distribution, row profile, drain timeline."""
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import numpy as np

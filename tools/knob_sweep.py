@@ -6,6 +6,7 @@ e.g.   python tools/knob_sweep.py 1:0,4:0,8:0 ';RTW_TAIL=100000;RTW_COOPG=16'
 (an empty setting = the defaults)
 """
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import torch

@@ -1,6 +1,7 @@
 """Developer tool: kernel time per Scene::hit strategy on small grids (waves
 mostly alone on their SIMD -> per-segment latency) and on the bench image."""
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import raytracing_in_a_weekend_rust_amd as rtw

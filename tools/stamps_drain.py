@@ -10,6 +10,7 @@ usage: RTW_LIB=raytracing_in_a_weekend_rust_amd/_lib/librtw_stamps.so \\
 """
 import ctypes as C
 import os
+os.environ.setdefault("RTW_AB", "1")  # the library reads tuning/diagnostic knobs only under RTW_AB
 import sys
 
 import numpy as np
