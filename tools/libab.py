@@ -12,6 +12,11 @@ import sys
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def libname(lib):
+    """ab/<name>/librtw.so -> <name>"""
+    return os.path.basename(os.path.dirname(os.path.abspath(lib))) or os.path.basename(lib)
+
+
 def main():
     rounds = int(sys.argv[1])
     libs = sys.argv[2:]
@@ -27,9 +32,9 @@ def main():
                 sys.exit(1)
             ms = json.loads(line[-1])["ms_per_step"]
             res[lib].append(ms)
-            print(f"round {r} {os.path.basename(lib)}: {ms:.2f} ms", flush=True)
+            print(f"round {r} {libname(lib)}: {ms:.2f} ms", flush=True)
     for lib, v in res.items():
-        print(f"{os.path.basename(lib)}: mean {sum(v) / len(v):.2f} ms  {['%.2f' % x for x in v]}")
+        print(f"{libname(lib)}: mean {sum(v) / len(v):.2f} ms  {['%.2f' % x for x in v]}")
 
 
 if __name__ == "__main__":
