@@ -104,6 +104,7 @@ def parse():
     p.add_argument("--pmc-out", default="",
                    help="also write the live PMC summary (stamped with the build id) to this JSON file")
     p.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    p.add_argument("--pmc-shard", default="", help=argparse.SUPPRESS)  # N:r -- the child renders rank r's rows
     a = p.parse_args()
     a.width, a.height = (int(v) for v in a.size.lower().split("x"))
     a.sim = tuple(int(v) for v in a.shard_of.split(":")) if a.shard_of else None
@@ -117,11 +118,17 @@ def workload_name(a):
 # ----------------------------------------------------------------- PMC leg --
 def pmc_child(a):
     """One frame of the workload through the one-shot ABI (the same launches as a
-    bench step), run under rocprofv3 --pmc by pmc_live()."""
+    bench step), run under rocprofv3 --pmc by pmc_live(); with --pmc-shard N:r only
+    rank r's rows of the N-rank row-cyclic split (the shard that rank renders)."""
     import raytracing_in_a_weekend_rust_amd as rtw
+    from raytracing_in_a_weekend_rust_amd import shard as sh
     cam, sph, ns, mt, nm = rtw.builtin_scene("complex", SEED, a.height, a.width, a.depth)
     one_shot = rtw.render_flat_fast if a.mode == "fast" else rtw.render_flat
-    one_shot(cam.raw, sph, ns, mt, nm, a.samples_sqrt, SEED)
+    rows = None
+    if a.pmc_shard:
+        n, r = (int(v) for v in a.pmc_shard.split(":"))
+        rows = sh.rows_of(r, n, a.height)
+    one_shot(cam.raw, sph, ns, mt, nm, a.samples_sqrt, SEED, shard=rows)
 
 
 def profiler_active():
@@ -159,9 +166,10 @@ def read_counters(d):
     return out
 
 
-def pmc_live(a, timeout_s=75):
+def pmc_live(a, timeout_s=75, shard=None):
     """Separate rocprofv3 --pmc passes over a one-frame child (no tracing in the same
-    run). Returns {pass: {kernel: {counter: value per dispatch}}} or None."""
+    run; `shard` = (N, r): the child renders rank r's rows only). Returns
+    {pass: {kernel: {counter: value per dispatch}}} or None."""
     exe = shutil.which("rocprofv3")
     if not exe or profiler_active():
         return None, "rocprofv3 not available" if not exe else "already under a profiler"
@@ -174,6 +182,8 @@ def pmc_live(a, timeout_s=75):
             cmd = [exe, "--pmc", *counters, "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--pmc-child", "--size", a.size,
                    "--samples-sqrt", str(a.samples_sqrt), "--depth", str(a.depth), "--mode", a.mode]
+            if shard:
+                cmd += ["--pmc-shard", f"{shard[0]}:{shard[1]}"]
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
                                  start_new_session=True, cwd=HERE)
             try:
@@ -496,9 +506,21 @@ def group_main(a, torch, rtw, shard):
                     "mean_wall_ms": round(sum(walls) / len(walls), 3),
                     "note": "root_gather_ms: GPU 0's stream from its own tile rendered to the image "
                             "complete (waiting for the slowest entry + gather + un-permute)"}
-    n_cu = torch.cuda.get_device_properties(devs[0]).multi_processor_count * len(set(devs))
-    out["roofline"] = roofline(a, total, info["render_ms_max"], max(p.main_kernel_ms for p in per),
-                               None, "not collected (N>1)", n_cu, total.grid_blocks)
+    # roofline of entry 0 (its rows of the split, its kernel time): the counter child
+    # renders the same rows on device 0
+    n_cu = torch.cuda.get_device_properties(devs[0]).multi_processor_count
+    pm, pm_source = None, "not collected (--pmc 0)"
+    if a.pmc and devs[0] == 0:
+        res, why = pmc_live(a, shard=(len(devs), 0))
+        kern = MAIN_KERNEL[a.mode]
+        if res and "insts" in res and kern in res["insts"]:
+            pm = pmc_summary(res, kern, rtw.build_id())
+            pm_source = f"live rocprofv3 --pmc passes of a child run of entry 0's rows of the x{len(devs)} split"
+        else:
+            pm_source = f"live PMC failed ({why})"
+    out["roofline"] = roofline(a, per[0], per[0].kernel_ms, per[0].main_kernel_ms, pm, pm_source, n_cu,
+                               per[0].grid_blocks)
+    out["roofline"]["scope"] = "entry 0 (device %d): its rows, its kernel time" % devs[0]
     out["parity"] = parity_check(a, image, total.segments)
     print(json.dumps(out), flush=True)
     g.close()
@@ -592,28 +614,31 @@ def main():
 
     out = None
     if rank == 0:
-        pm, pm_source = None, "not collected (N>1)"
+        pm, pm_source = None, "not collected (--pmc 0)"
         n_cu = torch.cuda.get_device_properties(local).multi_processor_count
-        if a.sim:
-            pm_source = "not collected (--shard-of: the counter child renders whole frames)"
-        elif world == 1:
-            if a.pmc:
-                res, why = pmc_live(a)
-                kern = MAIN_KERNEL[a.mode]
-                if res and "insts" in res and kern in res["insts"]:
-                    pm, pm_source = pmc_summary(res, kern, rtw.build_id()), "live rocprofv3 --pmc passes of a one-frame child run (this bench)"
-                    if a.pmc_out:
-                        with open(a.pmc_out, "w") as f:
-                            json.dump({**pm, "workload": workload_name(a), "mode": a.mode}, f, indent=1)
-                elif res and "insts" in res:  # the passes ran but matched no counters to the kernel
-                    seen = sorted({k for p in res.values() for k in p})
-                    pm_source = (f"live PMC passes ran but held no counters for kernel {kern} "
-                                 f"(kernels seen: {', '.join(seen[:8])}): frac/traffic not measured")
-                else:
-                    pm_source = f"live PMC failed ({why})"
-            if pm is None and a.mode == "parity" and workload_name(a) == "complex_1200x675_s23_d50":
-                pm, fb_why = pmc_fallback(MAIN_KERNEL[a.mode], rtw.build_id())
-                pm_source = (pm_source + "; " if a.pmc else "") + fb_why
+        # the counter child renders what this rank rendered: the whole frame (N=1, or
+        # weak scaling: rank 0's frame), or rank 0's rows of the strong split (the
+        # other ranks wait at the final barrier meanwhile)
+        child_shard = a.sim if a.sim else ((world, 0) if world > 1 and not weak else None)
+        what = ("a one-frame child run" if child_shard is None else
+                f"a child run of rank {child_shard[1]}'s rows of the x{child_shard[0]} split")
+        if a.pmc:
+            res, why = pmc_live(a, shard=child_shard)
+            kern = MAIN_KERNEL[a.mode]
+            if res and "insts" in res and kern in res["insts"]:
+                pm, pm_source = pmc_summary(res, kern, rtw.build_id()), f"live rocprofv3 --pmc passes of {what} (this bench)"
+                if a.pmc_out:
+                    with open(a.pmc_out, "w") as f:
+                        json.dump({**pm, "workload": workload_name(a), "mode": a.mode, "shard": child_shard}, f, indent=1)
+            elif res and "insts" in res:  # the passes ran but matched no counters to the kernel
+                seen = sorted({k for p in res.values() for k in p})
+                pm_source = (f"live PMC passes ran but held no counters for kernel {kern} "
+                             f"(kernels seen: {', '.join(seen[:8])}): frac/traffic not measured")
+            else:
+                pm_source = f"live PMC failed ({why})"
+        if pm is None and a.mode == "parity" and workload_name(a) == "complex_1200x675_s23_d50" and child_shard is None:
+            pm, fb_why = pmc_fallback(MAIN_KERNEL[a.mode], rtw.build_id())
+            pm_source = (pm_source + "; " if a.pmc else "") + fb_why
         out = base_line(a, value, elapsed, world, frames, ns)
         out["config"]["parallelism"] = (f"rank {a.sim[1]} of a row-cyclic x{a.sim[0]} split, alone on one "
                                         "GPU (value = this rank's samples / its time; the other ranks "
