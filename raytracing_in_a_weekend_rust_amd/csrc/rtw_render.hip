@@ -79,18 +79,6 @@ constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 s
                                             // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
-// Hand-out lists (cost order): one per XCD. Workgroups b and b + 8 share an XCD (round-robin
-// placement, MI355X_MICROARCH.md: a speed hint, never relied on for correctness), so a wave
-// starts on list (blockIdx.x % kLists) and moves to the next list when it runs dry. A list
-// holds whole 16-pixel column pairs of 8x8 tiles -- 384 B of an f64 row, three 128-B cache
-// lines -- so every framebuffer line is written by one XCD and its partial writes merge in
-// that XCD's L2 before the write-back (pixels of one line written from several XCDs each
-// went to HBM as their own 32-B sectors: 40 MB of writes for a 19.4 MB framebuffer).
-constexpr uint32_t kLists = 8;
-constexpr uint32_t kListStride = 16;  // u32 words between list cursor words (64 B apart)
-constexpr uint32_t kListWord0 = 32;   // first list word in the session's control block
-constexpr uint32_t kCtlWords = kListWord0 + kListStride * kLists;
-constexpr uint32_t kCtlPixelsDone = 3;  // control block word of pixels_done
 
 // Scene::hit strategies (one kernel instantiation each)
 constexpr int kScanF64 = 0;  // the reference's scan, f64 only
@@ -168,8 +156,6 @@ struct KParams {
     uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
                                 // segments is parked before its first sample (0: off)
-    uint32_t n_lists;           // hand-out lists (kLists with the cost order, else 1): list L holds
-                                // the tiles of cache-line-aligned 16-pixel column pairs assigned to it
     uint64_t seed_lo, seed_hi;
     const double4 *sph;         // {cx, cy, cz, r} f64 (the reference's values; r*r formed at each
                                 // use, as sphere.rs:49 does)
@@ -198,16 +184,11 @@ struct KParams {
     uint32_t *cost;             // per 8x8 tile: probe segments, then its bucket, then its base;
                                 // then per tile: its hot pixels
     uint32_t *pcost;            // per pixel: probe segments
-    uint32_t *cost_hist;        // [kLists][kCostBuckets] counts, then bucket write cursors; then
-                                // list_base
-    const uint32_t *list_base;  // [n_lists + 1]: list L = order_map[list_base[L], list_base[L + 1])
-    uint32_t *pix_cursor;       // list L's cursor word at pix_cursor + kListStride * L: a u64 of the
-                                // tickets handed out (low) and the pixels finished by its refills
-                                // (high)
+    uint32_t *cost_hist;        // [kCostBuckets] counts, then bucket write cursors
+    uint32_t *pix_cursor;       // next pixel of the persistent phase 1
     uint32_t *park_ctl_done;    // cursor-taking waves that will park no more
     uint32_t *park_flag;        // per park slot: 1 once the entry is published
-    uint32_t *pixels_done;      // pixels written outside the list words (drains, leftovers, after the
-                                // cursor ran dry); rtw_latch_check_lists adds the list words into it
+    uint32_t *pixels_done;      // pixels written (completeness check of the persistent kernel)
     uint32_t *park_processed;   // park entries finished (persistent drain + leftover launch)
     uint32_t *leftover_cursor;  // slot cursor of the leftover launch (rtw_park_leftover)
     uint64_t spin_guard;        // idle waits end after this many 100 MHz ticks without progress
@@ -337,40 +318,22 @@ constexpr uint32_t kRegSlots = 8;
 __device__ __forceinline__ uint64_t spill_idx(uint32_t level, uint64_t col, uint64_t stride) {
     return col * stride + (level - kRegSlots);
 }
-// Deferred runs: a push of the sphere the path hit last (prev == v: the bounce before
-// pushed v at level n-1) at a spill level is not written -- levels [w, n) are then
-// copies of level w-1, a run the path keeps in its depth word alone. The run is
-// written out when a different sphere is pushed, and read as level w-1's value by
-// the fold. A path trapped inside a sphere (L S S S ... to the depth cap) ends black
-// and is never folded (KParams::att_finite), so its run is never written: the spill
-// writes of the trapped paths (most of the persistent kernel's HBM writes) go away.
-// The stack's contents as the fold sees them are unchanged.
 struct PathStack {
     uint64_t r0 = 0, r1 = 0;
-    uint32_t nw = kRegSlots << 16;  // (w: levels written, >= kRegSlots) << 16 | n: depth
-    __device__ __forceinline__ uint32_t size() const { return nw & 0xffffu; }
-    __device__ __forceinline__ uint32_t written() const { return nw >> 16; }
-    // level w-1, the value of the deferred levels [w, n)
-    __device__ __forceinline__ uint32_t run_value(const uint16_t *spill, uint64_t stride, uint64_t col) const {
-        const uint32_t w = written();
-        return w == kRegSlots ? static_cast<uint32_t>(r1 >> 48) : spill[spill_idx(w - 1u, col, stride)];
-    }
-    __device__ __forceinline__ void push(uint32_t v, int prev, uint16_t *spill, uint64_t stride, uint64_t col) {
-        const uint32_t n = size();
+    uint32_t n = 0;
+    __device__ __forceinline__ void push(uint32_t v, uint16_t *spill, uint64_t stride, uint64_t col) {
         if (n < 4) r0 |= static_cast<uint64_t>(v) << (16u * n);
         else if (n < kRegSlots) r1 |= static_cast<uint64_t>(v) << (16u * (n - 4u));
-        else if (static_cast<int>(v) != prev) {  // not a copy of level n-1: write the run, then v
-            const uint32_t w = written();
-            if (w < n) {
-                const uint16_t x = static_cast<uint16_t>(run_value(spill, stride, col));
-                for (uint32_t j = w; j < n; ++j) spill[spill_idx(j, col, stride)] = x;
-            }
-            spill[spill_idx(n, col, stride)] = static_cast<uint16_t>(v);
-            nw = (n + 1u) << 16 | n;
-        }
-        ++nw;
+        else spill[spill_idx(n, col, stride)] = static_cast<uint16_t>(v);
+        ++n;
     }
-    __device__ __forceinline__ void clear() { r0 = r1 = 0, nw = kRegSlots << 16; }
+    __device__ __forceinline__ uint32_t at(uint32_t j, const uint16_t *spill, uint64_t stride,
+                                           uint64_t col) const {
+        if (j < 4) return static_cast<uint32_t>(r0 >> (16u * j)) & 0xffffu;
+        if (j < kRegSlots) return static_cast<uint32_t>(r1 >> (16u * (j - 4u))) & 0xffffu;
+        return spill[spill_idx(j, col, stride)];
+    }
+    __device__ __forceinline__ void clear() { r0 = r1 = 0, n = 0; }
 };
 
 // Diagnostic build only (-DRTW_STAMPS, librtw_stamps.so): per-wave s_memtime
@@ -686,7 +649,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
         const double w = -__builtin_sqrt(__builtin_fabs(1. - (qx * qx + qy * qy + qz * qz)));
         ndx = qx + nx * w, ndy = qy + ny * w, ndz = qz + nz * w;
     }
-    if (kind != RTW_DIELECTRIC) p.stk.push(static_cast<uint32_t>(best), p.prev, spill, stride, col);  // attenuation row
+    if (kind != RTW_DIELECTRIC) p.stk.push(static_cast<uint32_t>(best), spill, stride, col);  // attenuation row
     p.ox = px, p.oy = py, p.oz = pz;
     p.dx = ndx, p.dy = ndy, p.dz = ndz;
     p.prev = best;
@@ -746,10 +709,9 @@ __device__ __forceinline__ uint32_t trap_forward(const double4 T, uint32_t rem, 
 // one short loop body per level instead of a three-way branch.
 __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, const uint16_t *spill,
                                      uint64_t col, uint64_t stride, double &lr, double &lg, double &lb) {
-    const uint32_t n = p.stk.size(), w = p.stk.written();
-    const uint32_t x = n > w ? p.stk.run_value(spill, stride, col) : 0u;  // deferred levels [w, n)
+    const uint32_t n = p.stk.n;
     for (uint32_t j = n; j-- > kRegSlots;) {
-        const ShadeRec &A = shd[j >= w ? x : spill[spill_idx(j, col, stride)]];
+        const ShadeRec &A = shd[spill[spill_idx(j, col, stride)]];
         lr = A.a0 * lr;
         lg = A.a1 * lg;
         lb = A.a2 * lb;
@@ -1123,12 +1085,8 @@ __device__ __forceinline__ uint32_t ld_rlx(uint32_t *p) {
 // it alone could finish -- a ticket it claimed stays published-but-unclaimed
 // (flag 1) and the leftover launch (rtw_park_leftover) finishes it. Progress
 // therefore never depends on every workgroup being resident at once.
-// Progress signature: list 0's word stands for the lists (every list moves while the
-// cursor runs; after that, parks and pixels_done do). A signature that misses progress
-// can only end a wait early: the leftover launch then finishes what it left.
 __device__ __forceinline__ uint32_t progress_sig(const KParams &P) {
-    return ld_rlx(P.park_count) + ld_rlx(P.pixels_done) + ld_rlx(P.pix_cursor) + ld_rlx(P.pix_cursor + 1) +
-           ld_rlx(P.park_ctl_done);
+    return ld_rlx(P.park_count) + ld_rlx(P.pixels_done) + ld_rlx(P.pix_cursor) + ld_rlx(P.park_ctl_done);
 }
 struct SpinGuard {
     uint64_t t0;
@@ -1444,13 +1402,6 @@ struct TileGrid {
         return min(kOrderTile, P.W - bx) * min(kOrderTile, P.n_rows - by);
     }
 };
-// the hand-out list of tile t: its 16-pixel column pair (tiles 2j, 2j + 1 of a tile row),
-// spread over the lists by a diagonal pattern so that every list samples the whole image
-__device__ __forceinline__ uint32_t tile_list(const KParams &P, const TileGrid &tg, uint32_t t) {
-    if (P.n_lists <= 1u) return 0u;
-    const uint32_t tx = t % tg.tx, ty = t / tg.tx;
-    return ((tx >> 1) + 3u * ty) % P.n_lists;
-}
 __device__ __forceinline__ uint32_t cost_bucket(uint32_t segs, uint32_t pixels) {
     const uint32_t per = static_cast<uint32_t>((8ull * segs) / (static_cast<uint64_t>(pixels) * kProbeSamples));
     return kCostBuckets - 1u - min(per, kCostBuckets - 1u);  // 1/8 segment per sample
@@ -1511,51 +1462,23 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_bucket(const KParams P) {
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     if (t >= tg.count()) return;
     const uint32_t np = tg.pixels(P, t) - P.cost[tg.count() + t];
-    const uint32_t b = tile_list(P, tg, t) * kCostBuckets + (np ? cost_bucket(P.cost[t], np) : 0u);
+    const uint32_t b = np ? cost_bucket(P.cost[t], np) : 0u;
     P.cost[t] = b;
     if (np) atomicAdd(P.cost_hist + b, np);
-}
-// a hot pixel's histogram slot: its tile's list, its own bucket
-__device__ __forceinline__ uint32_t hot_slot(const KParams &P, uint64_t i) {
-    const TileGrid tg(P);
-    const uint32_t lr = static_cast<uint32_t>(i / P.W), x = static_cast<uint32_t>(i - static_cast<uint64_t>(lr) * P.W);
-    return tile_list(P, tg, tg.of(x, lr)) * kCostBuckets + cost_bucket(P.pcost[i], 1u);
 }
 // per hot pixel: its own bucket into the histogram
 __global__ __launch_bounds__(kBlock) void rtw_cost_hot_bucket(const KParams P) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
-    atomicAdd(P.cost_hist + hot_slot(P, i), 1u);
+    atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u);
 }
-// exclusive prefix sums of pixel counts over (list, bucket), list-major -> bucket write
-// cursors; list L's range of the order starts at list_base[L]. One workgroup of 64
-// threads: thread L sums its list, thread 0 the lists, thread L its list's buckets.
-__global__ __launch_bounds__(64) void rtw_cost_scan(const KParams P) {
-    __shared__ uint32_t tot[kLists + 1];
-    const uint32_t l = threadIdx.x;
-    uint32_t *h = P.cost_hist + static_cast<size_t>(l) * kCostBuckets;
-    if (l < P.n_lists) {
+// exclusive prefix sums of pixel counts over the buckets -> bucket write cursors
+__global__ void rtw_cost_scan(const KParams P) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
         uint32_t acc = 0;
-        for (uint32_t b = 0; b < kCostBuckets; ++b) acc += h[b];
-        tot[l] = acc;
-    }
-    __syncthreads();
-    if (l == 0) {
-        uint32_t *base = P.cost_hist + static_cast<size_t>(kLists) * kCostBuckets;  // = list_base
-        uint32_t acc = 0;
-        for (uint32_t k = 0; k < P.n_lists; ++k) {
-            const uint32_t c = tot[k];
-            tot[k] = acc, base[k] = acc;
-            acc += c;
-        }
-        base[P.n_lists] = acc;
-    }
-    __syncthreads();
-    if (l < P.n_lists) {
-        uint32_t acc = tot[l];
         for (uint32_t b = 0; b < kCostBuckets; ++b) {
-            const uint32_t c = h[b];
-            h[b] = acc;
+            const uint32_t c = P.cost_hist[b];
+            P.cost_hist[b] = acc;
             acc += c;
         }
     }
@@ -1572,7 +1495,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_place(const KParams P) {
 __global__ __launch_bounds__(kBlock) void rtw_cost_hot_place(const KParams P) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
     if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
-    P.order_map[atomicAdd(P.cost_hist + hot_slot(P, i), 1u)] = static_cast<uint32_t>(i);
+    P.order_map[atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u)] = static_cast<uint32_t>(i);
 }
 // one wave per tile (lane = row-major rank in the tile): order[tile base + rank
 // among the tile's non-hot pixels] = pixel
@@ -1669,8 +1592,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         }
                         continue;
                     }
-                    // list 0's hand-out for the lists' (they drain at one rate)
-                    if (static_cast<uint64_t>(ld_rlx(P.pix_cursor)) * P.n_lists >= P.join_at) {
+                    if (ld_rlx(P.pix_cursor) >= P.join_at) {
                         state = 2;
                         break;
                     }
@@ -1703,20 +1625,10 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         bool need = true;  // lane holds no pixel
         bool dry = false;  // wave-uniform: the cursor ran dry
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
-        // a pixel finished before the cursor ran dry is counted by the lane's next refill:
-        // a list's cursor and its count share one 64-bit word (tickets low, pixels high),
-        // so one atomic hands out the tickets and posts the completions (0.75 M
-        // completion atomics per frame fewer, 32 B of HBM writes each). A lane that
-        // finished its pixel is one whose ps.k reached n_off (a refill resets ps.k):
-        // no flag held across the loop.
-        // the hand-out list the wave takes tickets from (wave-uniform): its XCD's first
-        // (lists left to try << 8) | the list: one wave-uniform word
-        uint32_t lstate = (KP(n_lists) << 8) | (blockIdx.x % KP(n_lists));
         uint32_t x = 0, lr = 0, pseg = 0;
         bool spec = false;  // spec_lds holds the state the lane's next unit vector draws from
         uint64_t pix = 0;
         PixelState ps;
-        ps.k = 0;
         Path p;
         for (;;) {
             {  // the wave's first active lane counts the wave-level iteration
@@ -1726,23 +1638,15 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             bool dry_now = false;
             if (need && !dry) {  // refill: one atomic for the wave's idle lanes
                 const uint64_t m = __ballot(1);
-                const uint64_t nd = P.endgame ? 0ull : static_cast<uint64_t>(__popcll(__ballot(ps.k >= KP(n_off))));
-                ps.k = 0;
                 const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
                 uint32_t base = 0;
-                const uint32_t lst = lstate & 0xffu;
-                if (rank == 0)
-                    base = static_cast<uint32_t>(atomicAdd(reinterpret_cast<unsigned long long *>(KP(pix_cursor) + kListStride * lst),
-                                                           (nd << 32) | static_cast<uint64_t>(__popcll(m))));
+                if (rank == 0) base = atomicAdd(KP(pix_cursor), static_cast<uint32_t>(__popcll(m)));
 #ifdef RTW_WALK_DIAG  // diagnostic build: device-scope atomics of the cursor loop
                 if (rank == 0) atomicAdd(&P.counters[16], 1ull);
 #endif
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
-                // list lst = tickets [lbeg, lend) of the order (one list: the whole shard)
-                uint64_t lbeg = 0, lend = npix;
-                if (KP(n_lists) > 1u) lbeg = KP(list_base)[lst], lend = KP(list_base)[lst + 1u];
-                const uint64_t ticket = lbeg + static_cast<uint64_t>(base) + rank;
-                if (ticket < lend) {
+                const uint64_t ticket = static_cast<uint64_t>(base) + rank;
+                if (ticket < npix) {
                     // hand-out order: by descending estimated cost (P.order_map,
                     // rtw_cost_probe), so the cheapest pixels fill the drain; else
                     // rows bottom-up when P.order == 1, or row-major
@@ -1765,8 +1669,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     spec = false;
                     if (KP(max_depth) == 0) {  // every sample black, no Scene::hit call
                         ps.k = KP(n_off);
-                        write_pixel(P, x, lr, ps);  // counted here: not again by the refill
-                        ps.k = 0;
+                        write_pixel(P, x, lr, ps);
                     } else if (P.prepark && order_map && KP(pcost)[pix] >= P.prepark) {
                         // a long serial chain by the probe's estimate: to a drain wave
                         // from its first sample
@@ -1785,11 +1688,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     dry_now = true;
                 }
             }
-            if (__any(dry_now)) {  // wave-uniform: this list ran dry, on to the next; all dry: done
-                const uint32_t nxt = (lstate & 0xffu) + 1u;
-                lstate = __builtin_amdgcn_readfirstlane((lstate & ~0xffu) - 0x100u + (nxt == KP(n_lists) ? 0u : nxt));
-                dry = (lstate >> 8) == 0u;
-            }
+            dry = dry || __any(dry_now);  // wave-uniform
             // endgame: once the cursor is dry and at most P.endgame pixels of the shard
             // are unfinished (about one per drain group), every lane parks its pixel
             // at its next sample boundary -- the last chains then run on a whole wave
@@ -1892,9 +1791,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
                 if (kind != RTW_DIELECTRIC) {  // the bounce's attenuation row
                     if (ended) cr = M.a0 * 0., cg = M.a1 * 0., cb = M.a2 * 0.;  // att x black
-                    else p.stk.push(static_cast<uint32_t>(best), p.prev, KP(spill), stride, gid);
+                    else p.stk.push(static_cast<uint32_t>(best), KP(spill), stride, gid);
 #ifdef RTW_WALK_DIAG
-                    if (!ended && p.stk.size() > kRegSlots) atomicAdd(&P.counters[18], 1ull);  // spill-level pushes
+                    if (!ended && p.stk.n > kRegSlots) atomicAdd(&P.counters[18], 1ull);  // spill-level pushes
 #endif
                 }
                 p.ox = hx, p.oy = hy, p.oz = hz;
@@ -1925,11 +1824,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                                        static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                // posted by the next refill; after the cursor ran dry, or with the endgame
-                // rule (small shards: pixels_done alone then counts every finished pixel),
-                // one completion-count atomic per wave
-                {
-                    const uint64_t dm = __ballot(done && (dry || P.endgame));
+                {  // one completion-count atomic per wave (write_pixel leaves it to us)
+                    const uint64_t dm = __ballot(done);
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
                         atomicAdd(KP(pixels_done), static_cast<uint32_t>(__popcll(dm)));
 #ifdef RTW_WALK_DIAG
@@ -2184,16 +2080,6 @@ template <typename T>
 __global__ void rtw_latch_check(const T *written, T expect, uint32_t *err) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && *written != expect) atomicAdd(err, 1u);
 }
-// persistent renders: the pixels the refills posted into the list words are added into
-// pixels_done (which the host then reads), then the same check
-__global__ void rtw_latch_check_lists(uint32_t *ctl, uint32_t n_lists, uint32_t expect, uint32_t *err) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        uint32_t v = ctl[kCtlPixelsDone];
-        for (uint32_t l = 0; l < n_lists; ++l) v += ctl[kListWord0 + kListStride * l + 1u];
-        ctl[kCtlPixelsDone] = v;
-        if (v != expect) atomicAdd(err, 1u);
-    }
-}
 
 // ------------------------------------------------------------------- probes --
 __global__ void probe_seeds(U128 seed, uint64_t first, uint64_t count, const uint4 *tab,
@@ -2240,8 +2126,7 @@ struct rtw_session {
     size_t spill_bytes = 0;
     Parked *d_park = nullptr;  // park queue, one slot per pixel of the largest shard so far
     size_t park_cap = 0;
-    uint32_t *d_park_ctl = nullptr;  // [0] parked count, [1] phase-2 cursor, [3] pixels done, [4] cursor waves done,
-                                     // [5] processed, [6] leftover cursor; [kListWord0 + kListStride L]: list L (u64)
+    uint32_t *d_park_ctl = nullptr;  // [0] parked count, [1] phase-2 cursor, [2] pixel cursor
     U128 *d_seeds = nullptr;         // per-pixel RNG children of the current shard
     uint32_t *d_park_flag = nullptr; // per park slot publish flags
     uint32_t *d_order = nullptr, *d_cost = nullptr, *d_cost_hist = nullptr;  // cost-ordered hand-out
@@ -2505,9 +2390,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     if (cam->img_height == 0 || cam->img_width == 0)
         throw rtw::Error(RTW_E_EMPTY_IMAGE, "image height and width must be > 0");  // camera.rs:267
     if (samples_sqrt > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "samples_sqrt > 65535");
-    // the path stack's depth word holds 16 bits (PathStack); the spill levels alone
-    // would take (max_depth - 8) x 4 B per persistent lane beyond that
-    if (cam->max_depth > 65535) throw rtw::Error(RTW_E_UNSUPPORTED, "max_depth > 65535");
     const uint64_t npix = static_cast<uint64_t>(cam->img_height) * cam->img_width;
     const uint32_t bits = bit_length(npix - 1);
     if (bits > static_cast<uint32_t>(rtw::kJumpBits)) throw rtw::Error(RTW_E_UNSUPPORTED, "image > 2^40 pixels");
@@ -2605,9 +2487,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.park = s->d_park;
     P.park_count = s->d_park_ctl;
     P.park_cursor = s->d_park_ctl + 1;
-    P.pix_cursor = s->d_park_ctl + kListWord0;  // list words, kListStride apart (64-bit aligned)
-    P.pixels_done = s->d_park_ctl + kCtlPixelsDone;
-    P.park_ctl_done = s->d_park_ctl + 4;
+    P.pix_cursor = s->d_park_ctl + 2;
+    P.park_ctl_done = s->d_park_ctl + 3;
+    P.pixels_done = s->d_park_ctl + 4;
     P.park_processed = s->d_park_ctl + 5;
     P.leftover_cursor = s->d_park_ctl + 6;
     {
@@ -2684,7 +2566,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     const bool use_lds = lds <= kLdsCap;
     if (!use_lds) lds = 0;
     HIPCHECK(hipMemsetAsync(s->d_counters, 0, kCounters * sizeof(unsigned long long), st));
-    HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, kCtlWords * sizeof(uint32_t), st));
+    HIPCHECK(hipMemsetAsync(s->d_park_ctl, 0, 8 * sizeof(uint32_t), st));
     HIPCHECK(hipEventRecord(s->ev0, st));
     P.order = 2;
     if (const char *e = kn.get("RTW_ORDER")) P.order = static_cast<uint32_t>(std::atoi(e));
@@ -2700,18 +2582,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
         // bottom-up, 0 row-major
         P.order_map = nullptr;
-        P.n_lists = 1, P.list_base = nullptr;
         if (P.order == 2 && mode == kBvh && P.max_depth > 0) {
             P.cost = s->d_cost, P.cost_hist = s->d_cost_hist, P.order_map = s->d_order, P.pcost = s->d_pcost;
-            // hand-out lists, one per XCD (RTW_LISTS=1 under RTW_AB: one global list)
-            P.n_lists = kLists;
-            if (const char *e = kn.get("RTW_LISTS")) P.n_lists = std::atoi(e) == 1 ? 1u : kLists;
-            P.list_base = s->d_cost_hist + kLists * kCostBuckets;
             const dim3 g1(static_cast<uint32_t>((npix + kBlock - 1) / kBlock));
             const TileGrid tg(P);
             const dim3 gt((tg.count() + kBlock - 1) / kBlock);
             const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
-            HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kLists * kCostBuckets * sizeof(uint32_t), st));
+            HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
             P.probe_sub = 1;
             if (const char *e = kn.get("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
@@ -2843,7 +2720,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         else hipLaunchKernelGGL((rtw_park_leftover<false, 64>), grid_l, dim3(kBlock), 0, st, P);
         HIPCHECK(hipGetLastError());
     }
-    hipLaunchKernelGGL(rtw_latch_check_lists, dim3(1), dim3(64), 0, st, s->d_park_ctl, P.n_lists,
+    hipLaunchKernelGGL(rtw_latch_check<uint32_t>, dim3(1), dim3(64), 0, st,
+                       static_cast<const uint32_t *>(P.pixels_done),
                        static_cast<uint32_t>(static_cast<uint64_t>(P.n_rows) * P.W), s->d_err);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipEventRecord(s->ev1, st));
@@ -3002,10 +2880,10 @@ void collect(rtw_session *s) {
     s->last.sphere_tests = c[0] * s->n_sph;
     s->last.kernel_ms = ms;
     s->last.main_kernel_ms = s->main_ev ? main_ms : ms;
-    uint32_t ctl[8] = {};  // [kCtlPixelsDone]: every pixel written (rtw_latch_check_lists)
+    uint32_t ctl[8] = {};
     HIPCHECK(hipMemcpy(ctl, s->d_park_ctl, sizeof ctl, hipMemcpyDeviceToHost));
-    if (ctl[3] != static_cast<uint32_t>(s->last.pixels))  // never a silently incomplete image
-        throw rtw::Error(RTW_E_HIP, "render incomplete: " + std::to_string(ctl[3]) + " of " +
+    if (ctl[4] != static_cast<uint32_t>(s->last.pixels))  // never a silently incomplete image
+        throw rtw::Error(RTW_E_HIP, "render incomplete: " + std::to_string(ctl[4]) + " of " +
                                         std::to_string(s->last.pixels) + " pixels written");
 }
 
@@ -3028,10 +2906,10 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev_k0));
         HIPCHECK(hipEventCreate(&s->ev_k1));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
-        HIPCHECK(hipMalloc(&s->d_park_ctl, kCtlWords * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_err, sizeof(uint32_t)));
         HIPCHECK(hipMemset(s->d_err, 0, sizeof(uint32_t)));
-        HIPCHECK(hipMalloc(&s->d_cost_hist, (kLists * kCostBuckets + kLists + 1) * sizeof(uint32_t)));
+        HIPCHECK(hipMalloc(&s->d_cost_hist, kCostBuckets * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_fcursor, sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_fcount, 8 * sizeof(unsigned long long)));
         HIPCHECK(hipDeviceGetAttribute(&s->n_cu, hipDeviceAttributeMultiprocessorCount, device));

@@ -2,7 +2,7 @@
 its own child run, no tracing), per kernel, for the main render kernel's
 diagnosis. Reuses bench.py's child and csv reader.
 
-usage: python tools/pmc_diag.py [--size WxH] [--samples-sqrt S] NAME=CTR,CTR,... [NAME=...]
+usage: python tools/pmc_diag.py [--size WxH] [--samples-sqrt S] [--mode fast] NAME=CTR,CTR,... [NAME=...]
        (env: RTW_LIB selects a library build, as for bench.py)
 prints one JSON object: {pass: {kernel: {counter: value per dispatch}}}
 """
@@ -30,6 +30,11 @@ def main():
         i = args.index("--samples-sqrt")
         s = args[i + 1]
         del args[i:i + 2]
+    mode = "parity"
+    if "--mode" in args:
+        i = args.index("--mode")
+        mode = args[i + 1]
+        del args[i:i + 2]
     exe = shutil.which("rocprofv3")
     out = {}
     tmp = tempfile.mkdtemp(prefix="rtw_pmcdiag_")
@@ -40,7 +45,7 @@ def main():
             d = os.path.join(tmp, name)
             cmd = [exe, "--pmc", *ctrs.split(","), "-d", d, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.join(HERE, "bench.py"), "--pmc-child", "--size", size,
-                   "--samples-sqrt", s]
+                   "--samples-sqrt", s, "--mode", mode]
             p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env,
                                  start_new_session=True, cwd=HERE)
             try:

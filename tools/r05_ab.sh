@@ -16,7 +16,7 @@ tail -$# $OUT/ab.log
 for S in "$@"; do
   L=${S%%@*}; E=""; [ "$S" != "$L" ] && E=${S#*@}
   N=$(basename $(dirname $L))${E:+_${E//[,=]/_}}
-  env ${E//,/ } RTW_LIB=$(realpath $L) timeout -k 10 300 python tools/pmc_diag.py write=WRITE_SIZE > $OUT/pmc_write_$N.json 2> $OUT/pmc_write_$N.err || echo "pmc $N failed"
+  env ${E//,/ } RTW_LIB=$(realpath $L) timeout -k 10 300 python tools/pmc_diag.py ${PMC_MODE:+--mode $PMC_MODE} write=WRITE_SIZE > $OUT/pmc_write_$N.json 2> $OUT/pmc_write_$N.err || echo "pmc $N failed"
   python3 -c "import json,sys;d=json.load(open('$OUT/pmc_write_$N.json'))['write'];print('$N', {k:round(v['WRITE_SIZE']*1024/1e6,1) for k,v in d.items() if v.get('WRITE_SIZE',0)>100})" || true
   if [ "${PMC_INSTS:-0}" = 1 ]; then
     env ${E//,/ } RTW_LIB=$(realpath $L) timeout -k 10 300 python tools/pmc_diag.py insts=SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_VALU,SQ_THREAD_CYCLES_VALU > $OUT/pmc_insts_$N.json 2> $OUT/pmc_insts_$N.err || echo "pmc insts $N failed"
