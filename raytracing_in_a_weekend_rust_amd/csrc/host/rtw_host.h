@@ -71,6 +71,12 @@ Color color_random(XorShift &r);  // color.rs:249-255
 // cols[k*128 + j] = T^(2^k)(e_j), k < kJumpBits.
 constexpr int kJumpBits = 40;
 const std::vector<u128> &jump_table();
+// The trapped-path replay's lane table (rtw_render.hip trap_forward): for each bit b of
+// a 128-bit state (b < 64: lo bit b, else hi bit b - 64) and lane j < 64,
+// tries[b * 64 + j] = T^(3 j)(e_b) -- lane j's RNG state at the start of the j-th
+// 3-draw try after a wave-uniform state s is the XOR over s's set bits. Row 128 is zero.
+constexpr int kTryLanes = 64;
+const std::vector<u128> &try_table();
 u128 jump(u128 state, uint64_t p);
 u128 copy_reset_of(u128 parent_state);  // child handed out by copy_reset at this parent state
 

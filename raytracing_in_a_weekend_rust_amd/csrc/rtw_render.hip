@@ -192,6 +192,7 @@ struct KParams {
     uint32_t *park_processed;   // park entries finished (persistent drain + leftover launch)
     uint32_t *leftover_cursor;  // slot cursor of the leftover launch (rtw_park_leftover)
     uint64_t spin_guard;        // idle waits end after this many 100 MHz ticks without progress
+    const uint4 *tries;         // trapped-path replay lane table (rtw::try_table, [129][64] columns)
     unsigned long long *counters;  // [0] segments, [1] wave iterations, [2] exact tests,
                                    // [3] wave exact-pass iterations, [4] walk visits, [5] brute segments,
                                    // [6] parked pixels, [7] idle waits ended by the no-progress guard,
@@ -657,13 +658,82 @@ __device__ __forceinline__ bool shade(const KParams &P, const double4 *__restric
     return p.depth >= P.max_depth;  // ray_color(depth >= max) -> black
 }
 
+// One 64-lane round of random_unit_vec tries (vec3.rs:219-232) after the wave-uniform
+// RNG state s: lane j takes try j -- the three draws after 3 j draws -- from its state
+// T^(3 j) s, the XOR of the try table's columns over s's set bits (rtw::try_table; s is
+// wave-uniform, so the bit loop is scalar and each step one coalesced 1-KB load). The
+// accept decision is random_unit_vec's, so the accepted tries of the round are, in lane
+// order, the unit vectors the serial loop would return, and a lane's state after its
+// draws is the serial loop's state after that try. Returns the ballot of accepted tries;
+// (ux, uy, uz) = the lane's unit vector, st = its state after its three draws.
+#ifndef RTW_TRY_GATHER
+#define RTW_TRY_GATHER 4
+#endif
+constexpr int kGather = RTW_TRY_GATHER;  // table columns loaded per trip of the gather loop
+__device__ __forceinline__ uint64_t unit_vec_round(const uint4 *__restrict__ tries, U128 s, U128 &st, double &ux,
+                                                   double &uy, double &uz) {
+    const uint32_t lane = __lane_id();
+    const uint4 *col = tries + lane;
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t h = 0; h < 2; ++h) {
+        uint64_t m = h ? s.hi : s.lo;
+        // (readfirstlane returns int: the low word goes through uint32_t, not sign-extended)
+        m = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m >> 32))))
+             << 32) |
+            static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m)));
+        const uint32_t off = h ? 64u : 0u;
+        while (m) {  // kGather columns per trip, their loads in flight together (row 128 is zero)
+            uint32_t b[kGather];
+#pragma unroll
+            for (int q = 0; q < kGather; ++q) {
+                b[q] = m ? static_cast<uint32_t>(__builtin_ctzll(m)) + off : 128u;
+                m &= m - 1ull;
+            }
+            uint4 c[kGather];
+#pragma unroll
+            for (int q = 0; q < kGather; ++q) c[q] = col[b[q] * 64u];
+#pragma unroll
+            for (int q = 0; q < kGather; ++q) {
+                lo ^= (static_cast<uint64_t>(c[q].y) << 32) | c[q].x;
+                hi ^= (static_cast<uint64_t>(c[q].w) << 32) | c[q].z;
+            }
+        }
+    }
+    st = U128{lo, hi};
+    const uint32_t m0 = xs_next_m(st), m1 = xs_next_m(st), m2 = xs_next_m(st);
+    const float x32 = coord32(m0), y32 = coord32(m1), z32 = coord32(m2);
+    const float l32 = fmaf(x32, x32, fmaf(y32, y32, z32 * z32));
+    const double x = coord64(m0), y = coord64(m1), z = coord64(m2);
+    const double l2 = x * x + y * y + z * z;
+    // random_unit_vec's decision: surely rejected in f32, else surely or exactly accepted
+    const bool ok = !(l32 > 1.f + kRejBand) && (l32 < 1.f - kRejBand || l2 <= 1.);
+    ux = x, uy = y, uz = z;
+    rtw_num::div3(ux, uy, uz, __builtin_sqrt(l2));  // x / l, y / l, z / l (random_unit_vec's)
+    return __ballot(ok);
+}
+__device__ __forceinline__ double readlane_f64(double v, uint32_t l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l) {
+    return (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l)))
+            << 32) |
+           static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v), l));
+}
+
 // Trapped-path fast-forward (rtw_accel.h "Trapped paths"). The path has just
 // scattered inside sphere S (record T) with `rem` segments left before the depth
 // cap. Returns rem if every one of them provably stays inside S -- the sample
 // then ends black, and for a Lambertian trap the RNG has advanced by the rem
 // random_unit_vec draws those bounces make -- or 0 with nothing changed.
+// kWave (64-lane drain groups: every lane of the wave holds this path): the draws are
+// replayed 64 tries at a time, one per lane (unit_vec_round), and the wave walks the
+// accepted ones in order -- the serial rejection loop (89 % of a Lambertian-trapped
+// chain's time in round 4) becomes a table gather per 64 tries.
+template <bool kWave = false>
 __device__ __forceinline__ uint32_t trap_forward(const double4 T, uint32_t rem, const TrapHint &th,
-                                                 double dx, double dy, double dz, U128 &rng) {
+                                                 double dx, double dy, double dz, U128 &rng,
+                                                 const uint4 *__restrict__ tries = nullptr) {
     const double cap = T.w;
     if (!(th.h0x * T.x + th.h0y * T.y + th.h0z * T.z < cap)) return 0u;  // the next chord's start
     if (th.tir) {
@@ -680,6 +750,37 @@ __device__ __forceinline__ uint32_t trap_forward(const double4 T, uint32_t rem, 
     if (!th.quirk && !(th.a1 >= 1e-9)) return 0u;
     // end of the next chord: c + r u, or the antipode when near_zero set d = n_in
     double hx = th.quirk ? -th.h0x : th.ux, hy = th.quirk ? -th.h0y : th.uy, hz = th.quirk ? -th.h0z : th.uz;
+    if constexpr (kWave) {
+        U128 base = rng;
+        uint32_t i = 1;  // the bounce whose chord end is checked next
+        for (;;) {
+            U128 st;
+            double ux, uy, uz;
+            uint64_t acc = unit_vec_round(tries, base, st, ux, uy, uz);
+            while (acc) {
+                const uint32_t a = static_cast<uint32_t>(__builtin_ctzll(acc));
+                acc &= acc - 1ull;
+                if (!(hx * T.x + hy * T.y + hz * T.z < cap)) return 0u;  // end of chord i
+                if (i >= rem) {  // the scatter at the end of segment rem: its draws are the last
+                    rng = U128{readlane_u64(st.lo, a), readlane_u64(st.hi, a)};
+                    return rem;
+                }
+                const double vx = readlane_f64(ux, a), vy = readlane_f64(uy, a), vz = readlane_f64(uz, a);
+                const double ex = vx - hx, ey = vy - hy, ez = vz - hz;
+                const bool q_yes = ex < -1e-6 && ey < -1e-6 && ez < -1e-6;
+                const bool q_no = ex > 1e-6 || ey > 1e-6 || ez > 1e-6;
+                if (q_yes == q_no) return 0u;
+                if (q_yes) {
+                    hx = -hx, hy = -hy, hz = -hz;
+                } else {
+                    if (!(ex * ex + ey * ey + ez * ez >= 1e-8)) return 0u;
+                    hx = vx, hy = vy, hz = vz;
+                }
+                ++i;
+            }
+            base = U128{readlane_u64(st.lo, 63u), readlane_u64(st.hi, 63u)};  // after the round's 64 tries
+        }
+    }
     U128 r2 = rng;
     for (uint32_t i = 1;; ++i) {
         if (!(hx * T.x + hy * T.y + hz * T.z < cap)) return 0u;  // end of chord i
@@ -740,7 +841,7 @@ __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, 
 // With kTrap (drain groups: one path per group, so the branch is uniform) a
 // path trapped inside a sphere is fast-forwarded to its depth cap (trap_forward);
 // `trapped` counts the segments skipped that way.
-template <bool kTrap = false, class HitFn>
+template <bool kTrap = false, bool kWave = false, class HitFn>
 __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView &sv,
                                               uint32_t x, uint32_t y, uint16_t *spill, uint64_t col,
                                               PixelState &ps, uint32_t budget, uint32_t &seg, Stamps &stp,
@@ -778,7 +879,8 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
             const bool skip = th.tir && best == tir_no;
             if (!skip) tir_no = -1;  // kept through a run of TIR bounces in the same S
             if (!done && (th.lam || th.tir) && !skip) {
-                const uint32_t k = trap_forward(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz, ps.rng);
+                const uint32_t k = trap_forward<kWave>(KP(trap)[best], P.max_depth - p.depth, th, p.dx, p.dy, p.dz,
+                                                       ps.rng, KP(tries));
                 if (!k && th.tir) tir_no = best;
                 if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
             }
@@ -1353,7 +1455,7 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         return best;
     };
     uint32_t s = 0, trapped = 0;
-    trace_samples<true>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    trace_samples<true, kG == 64>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
     if (sub == 0) tl.trap += trapped;
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
@@ -2121,6 +2223,7 @@ struct rtw_session {
     uint32_t n_nbr = 0;
     double4 *d_trap = nullptr;  // per-sphere trapped-path records
     uint4 *d_jump = nullptr;
+    uint4 *d_tries = nullptr;  // rtw::try_table (trapped-path replay, 129 x 64 columns)
     unsigned long long *d_counters = nullptr;
     uint16_t *d_spill = nullptr;
     size_t spill_bytes = 0;
@@ -2180,6 +2283,15 @@ void upload_jump(rtw_session *s) {
     }
     HIPCHECK(hipMalloc(&s->d_jump, cols.size() * sizeof(uint4)));
     HIPCHECK(hipMemcpy(s->d_jump, cols.data(), cols.size() * sizeof(uint4), hipMemcpyHostToDevice));
+    const auto &tt = rtw::try_table();
+    std::vector<uint4> tc(tt.size());
+    for (size_t i = 0; i < tt.size(); ++i) {
+        const uint64_t lo = static_cast<uint64_t>(tt[i]), hi = static_cast<uint64_t>(tt[i] >> 64);
+        tc[i] = make_uint4(static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32), static_cast<uint32_t>(hi),
+                           static_cast<uint32_t>(hi >> 32));
+    }
+    HIPCHECK(hipMalloc(&s->d_tries, tc.size() * sizeof(uint4)));
+    HIPCHECK(hipMemcpy(s->d_tries, tc.data(), tc.size() * sizeof(uint4), hipMemcpyHostToDevice));
 }
 
 void validate_scene(const rtw_sphere *sp, uint32_t n, const rtw_material *m, uint32_t nm) {
@@ -2443,6 +2555,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
     P.n_nbr = s->n_nbr;
     P.trap = s->d_trap;
     P.jump = s->d_jump;
+    P.tries = s->d_tries;
     P.out = out;
     // path-stack spill levels: (max_depth - kRegSlots) x pixels x u16, grown on demand
     // path-stack spill: 2 regions x (max_depth - kRegSlots) levels x columns (u16);
@@ -3064,7 +3177,7 @@ int rtw_session_destroy(rtw_session *s) {
     (void)hipSetDevice(s->device);
     if (s->pending && s->ev1) (void)hipEventSynchronize(s->ev1);
     dev_free(s->d_arena), dev_free(s->d_out);  // the scene tables point into the arena
-    dev_free(s->d_jump), dev_free(s->d_counters), dev_free(s->d_spill);
+    dev_free(s->d_jump), dev_free(s->d_tries), dev_free(s->d_counters), dev_free(s->d_spill);
     dev_free(s->d_park), dev_free(s->d_park_ctl), dev_free(s->d_seeds), dev_free(s->d_diag);
     dev_free(s->d_park_flag), dev_free(s->d_order), dev_free(s->d_cost), dev_free(s->d_cost_hist);
     dev_free(s->d_pcost), dev_free(s->d_err);
