@@ -27,7 +27,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra 
 LIB_SRCS := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/host/*.cpp $(SRC)/host/*.h)) include/rtw_capi.h
 BUILD_ID := $(shell cat $(LIB_SRCS) | sha256sum | cut -c1-12)-$(shell echo '$(ARCH) $(HIPFLAGS)' | sha256sum | cut -c1-4)
 
-all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check $(OUT)/try_check
 
 $(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
@@ -51,6 +51,10 @@ $(OUT)/rtw_accel_build.o: $(SRC)/host/rtw_accel_build.cpp $(SRC)/rtw_accel.h
 $(OUT)/next01_check: tools/next01_check.cpp $(SRC)/rtw_numeric.h
 	@mkdir -p $(OUT)
 	$(CXX) -O2 -std=c++17 -ffp-contract=off -fno-fast-math -I$(SRC) -o $@ $< -lpthread
+
+# test infrastructure: host emulation of the trapped-path replay vs the serial draws (tests/test_accel.py)
+$(OUT)/try_check: tools/try_check.cpp $(SRC)/rtw_numeric.h $(OUT)/librtw.so
+	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/try_check.cpp -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
 
 # test infrastructure: host self-check of the BVH walk (tests/test_accel.py)
 $(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so

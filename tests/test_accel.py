@@ -92,3 +92,17 @@ def test_square_root_free_total_internal_reflection_test():
     assert p.returncode == 0, p.stdout + p.stderr
     r = json.loads(p.stdout)
     assert r["mismatches"] == 0 and r["tir_checked"] > 40_000_000
+
+
+def test_trapped_path_replay_matches_serial_draws():
+    """The drain groups' trapped-path replay (rtw_render.hip unit_vec_round: lane j of a
+    64-lane round draws try j from T^(3j) of the base state, via rtw::try_table) yields
+    the serial random_unit_vec loop's unit vectors (vec3.rs:219-232) and RNG states, in
+    order, over 2000 random states x 70 vectors (host emulation of the device code)."""
+    exe = os.path.join(ROOT, "raytracing_in_a_weekend_rust_amd", "_lib", "try_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", ROOT, "-j8", "all"], check=True, capture_output=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout + p.stderr
+    r = json.loads(p.stdout)
+    assert r["mismatches"] == 0 and r["checked"] == 140000
