@@ -1553,9 +1553,25 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
             }
         }
         P.pcost[i] = segs;
+        // the tile's cost word (hot pixels: its hot count), summed over the wave's lanes
+        // that share it before one atomic per word: consecutive lanes hold consecutive
+        // pixels, so a wave touches ~9 tile words -- one device-scope atomic (32 B of HBM
+        // writes) per word instead of one per pixel (25 MB a frame)
         const TileGrid tg(P);
-        if (segs >= kHotSegs) atomicAdd(P.cost + tg.count() + tg.of(x, lr), 1u);
-        else atomicAdd(P.cost + tg.of(x, lr), segs * wgt);
+        const bool hot = segs >= kHotSegs;
+        const uint32_t key = (hot ? tg.count() : 0u) + tg.of(x, lr);
+        const uint32_t val = hot ? 1u : segs * wgt;
+        const uint32_t lane = __lane_id();
+        for (uint64_t todo = __ballot(1); todo;) {  // the active lanes, one tile word per trip
+            const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(todo));
+            const uint32_t k = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(key), leader));
+            const uint64_t grp = __ballot(key == k) & todo;
+            uint32_t v = 0;  // the group's values by lane reads (only active lanes are read)
+            for (uint64_t g = grp; g; g &= g - 1ull)
+                v += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(val), __builtin_ctzll(g)));
+            if (lane == leader) atomicAdd(P.cost + k, v);
+            todo &= ~grp;
+        }
     }
 }
 // per tile: cost bucket of its non-hot pixels and their count into the histogram
