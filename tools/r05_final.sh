@@ -27,4 +27,5 @@ cat $OUT/bench_fast.json
 timeout -k 10 400 python tools/shard_time.py 1 2 4 8 > $OUT/shard_time.log 2>&1
 grep "^N=" $OUT/shard_time.log
 timeout -k 10 300 python tools/config12.py > $OUT/config12.json 2>&1
+timeout -k 10 300 python bench.py --shard-of 8:4 --steps 3 --cpu-baseline 0 --e2e 0 > $OUT/bench_shard8_4.json 2> $OUT/bench_shard8_4.err
 cat $OUT/config12.json
