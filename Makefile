@@ -27,7 +27,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra 
 LIB_SRCS := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/host/*.cpp $(SRC)/host/*.h)) include/rtw_capi.h
 BUILD_ID := $(shell cat $(LIB_SRCS) | sha256sum | cut -c1-12)-$(shell echo '$(ARCH) $(HIPFLAGS)' | sha256sum | cut -c1-4)
 
-all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check $(OUT)/try_check
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check $(OUT)/try_check $(OUT)/defer_model
 
 $(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
@@ -59,6 +59,10 @@ $(OUT)/try_check: tools/try_check.cpp $(SRC)/rtw_numeric.h $(OUT)/librtw.so
 # test infrastructure: host self-check of the BVH walk (tests/test_accel.py)
 $(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
 	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/accel_check.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
+
+# developer tool: host model of the lane-compacted leaf pass (RTW_DEFER_LEAVES builds)
+$(OUT)/defer_model: tools/defer_model.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
+	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/defer_model.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
 
 # rewritten only when the id changes (so an unchanged tree rebuilds nothing)
 $(OUT)/rtw_build_id.h: FORCE

@@ -39,9 +39,12 @@ def main():
             if p.returncode != 0 or not line:
                 print(f"{lib}: failed rc={p.returncode}\n{p.stderr[-2000:]}", flush=True)
                 sys.exit(1)
-            ms = json.loads(line[-1])["ms_per_step"]
+            d = json.loads(line[-1])
+            ms = d["ms_per_step"]
             res[lib].append(ms)
-            print(f"round {r} {libname(lib)}: {ms:.2f} ms", flush=True)
+            par = (d.get("parity") or {}).get("fb_sha256_ok")
+            visits = (d.get("stats") or {}).get("node_visits_per_segment")
+            print(f"round {r} {libname(lib)}: {ms:.2f} ms  parity {par}  visits/seg {visits}", flush=True)
     for lib, v in res.items():
         print(f"{libname(lib)}: mean {sum(v) / len(v):.2f} ms  {['%.2f' % x for x in v]}")
 
