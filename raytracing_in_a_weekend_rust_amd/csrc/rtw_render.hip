@@ -149,6 +149,8 @@ struct KParams {
     uint32_t endgame;           // dry cursor and at most this many pixels unfinished: park at the
                                 // next sample boundary (0: off)
     uint32_t probe_sub;         // cost probe on every probe_sub-th pixel of every probe_sub-th row
+    uint32_t probe_cap;         // cost probe: segments traced per probe sample at most
+    uint32_t hot_segs;          // cost probe: a pixel with >= hot_segs probe segments is ordered alone
     uint32_t drain_off;         // tests (RTW_DRAIN_OFF=1): the persistent kernel drains no parked
                                 // pixel; the leftover launch finishes them all
     uint32_t drain_prio;        // draining waves' issue priority after the cursor phase (RTW_DRAIN_PRIO,
@@ -1551,6 +1553,7 @@ __device__ __forceinline__ const float4 *stage_filt(const KParams &P, float4 *lf
 // refilled together get neighbouring pixels (coherent rays).
 constexpr uint32_t kProbeSamples = 2;
 constexpr uint32_t kHotSegs = kProbeSamples * 10;  // probe segments: >= 10 per sample
+constexpr uint32_t kProbeCap = 8;  // probe segments per sample at most
 constexpr uint32_t kCostBuckets = 256;
 constexpr uint32_t kOrderTile = 8;
 struct TileGrid {
@@ -1602,14 +1605,15 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
             Path p;
             gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p, stp);
-            for (;;) {  // one path (no spill: depth capped below the register slots)
+            for (;;) {  // one path, at most probe_cap segments (only counted: no attenuation rows kept)
                 ++segs;
                 const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
                 double bt = 0.;
                 const int best = bvh_hit<kLds, kProbeBlock>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
-                if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= kRegSlots) break;
+                if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= P.probe_cap) break;
                 double cr, cg, cb;
                 shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
+                p.stk.clear();  // the register slots never fill, whatever the cap
             }
         }
         P.pcost[i] = segs;
@@ -1618,7 +1622,7 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         // pixels, so a wave touches ~9 tile words -- one device-scope atomic (32 B of HBM
         // writes) per word instead of one per pixel (25 MB a frame)
         const TileGrid tg(P);
-        const bool hot = segs >= kHotSegs;
+        const bool hot = segs >= P.hot_segs;
         const uint32_t key = (hot ? tg.count() : 0u) + tg.of(x, lr);
         const uint32_t val = hot ? 1u : segs * wgt;
         const uint32_t lane = __lane_id();
@@ -1634,20 +1638,46 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         }
     }
 }
+// Per-wave aggregation of histogram atomics: neighbouring tiles fall in few buckets,
+// so one atomic per distinct bucket of the wave instead of one per tile (the 256
+// counters were contended: 46-48 us per kernel and frame). Returns the base the
+// bucket's atomic returned plus the counts of the lanes below in the same bucket.
+__device__ __forceinline__ uint32_t hist_add_wave(uint32_t *hist, uint32_t key, uint32_t val, bool on) {
+    const uint32_t lane = __lane_id();
+    uint32_t mine = 0;
+    for (uint64_t todo = __ballot(on); todo;) {  // wave-uniform trips, one bucket each
+        const uint32_t leader = static_cast<uint32_t>(__builtin_ctzll(todo));
+        const uint32_t k = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(key), leader));
+        const uint64_t grp = __ballot(on && key == k) & todo;
+        uint32_t tot = 0, below = 0;
+        for (uint64_t g = grp; g; g &= g - 1ull) {
+            const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(g));
+            const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(val), l));
+            below += l < lane ? v : 0u;
+            tot += v;
+        }
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(hist + k, tot);
+        base = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base), leader));
+        if ((grp >> lane) & 1ull) mine = base + below;
+        todo &= ~grp;
+    }
+    return mine;
+}
 // per tile: cost bucket of its non-hot pixels and their count into the histogram
 __global__ __launch_bounds__(kBlock) void rtw_cost_bucket(const KParams P) {
     const TileGrid tg(P);
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= tg.count()) return;
-    const uint32_t np = tg.pixels(P, t) - P.cost[tg.count() + t];
+    const bool in = t < tg.count();
+    const uint32_t np = in ? tg.pixels(P, t) - P.cost[tg.count() + t] : 0u;
     const uint32_t b = np ? cost_bucket(P.cost[t], np) : 0u;
-    P.cost[t] = b;
-    if (np) atomicAdd(P.cost_hist + b, np);
+    if (in) P.cost[t] = b;
+    hist_add_wave(P.cost_hist, b, np, np != 0u);
 }
 // per hot pixel: its own bucket into the histogram
 __global__ __launch_bounds__(kBlock) void rtw_cost_hot_bucket(const KParams P) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
+    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < P.hot_segs) return;
     atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u);
 }
 // exclusive prefix sums of pixel counts over the buckets -> bucket write cursors
@@ -1665,14 +1695,15 @@ __global__ void rtw_cost_scan(const KParams P) {
 __global__ __launch_bounds__(kBlock) void rtw_cost_place(const KParams P) {
     const TileGrid tg(P);
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    if (t >= tg.count()) return;
-    const uint32_t np = tg.pixels(P, t) - P.cost[tg.count() + t];
-    if (np) P.cost[t] = atomicAdd(P.cost_hist + P.cost[t], np);
+    const bool in = t < tg.count();
+    const uint32_t np = in ? tg.pixels(P, t) - P.cost[tg.count() + t] : 0u;
+    const uint32_t base = hist_add_wave(P.cost_hist, in ? P.cost[t] : 0u, np, np != 0u);
+    if (np) P.cost[t] = base;
 }
 // per hot pixel: its slot in the order
 __global__ __launch_bounds__(kBlock) void rtw_cost_hot_place(const KParams P) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x;
-    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < kHotSegs) return;
+    if (i >= static_cast<uint64_t>(P.n_rows) * P.W || P.pcost[i] < P.hot_segs) return;
     P.order_map[atomicAdd(P.cost_hist + cost_bucket(P.pcost[i], 1u), 1u)] = static_cast<uint32_t>(i);
 }
 // one wave per tile (lane = row-major rank in the tile): order[tile base + rank
@@ -1685,7 +1716,7 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
     const uint32_t wx = min(kOrderTile, P.W - bx), wy = min(kOrderTile, P.n_rows - by);
     const uint32_t x = bx + r % wx, lr = by + r / wx;
     const uint64_t i = static_cast<uint64_t>(lr) * P.W + x;
-    const bool mine = r < wx * wy && P.pcost[i] < kHotSegs;
+    const bool mine = r < wx * wy && P.pcost[i] < P.hot_segs;
     const uint64_t m = __ballot(mine);
     if (mine) P.order_map[P.cost[t] + static_cast<uint32_t>(__popcll(m & ((1ull << r) - 1ull)))] = static_cast<uint32_t>(i);
 }
@@ -2784,6 +2815,9 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
             P.probe_sub = 1;
             if (const char *e = kn.get("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+            P.probe_cap = kProbeCap, P.hot_segs = kHotSegs;
+            if (const char *e = kn.get("RTW_PROBE_CAP")) P.probe_cap = static_cast<uint32_t>(std::max(1, std::atoi(e)));
+            if (const char *e = kn.get("RTW_HOT_SEGS")) P.hot_segs = static_cast<uint32_t>(std::max(1, std::atoi(e)));
             if (P.probe_sub > 1) HIPCHECK(hipMemsetAsync(s->d_pcost, 0, npix * sizeof(uint32_t), st));
             // probe: scene + per-lane walk stacks in LDS when they fit, one workgroup per CU
             KParams Q = P;
@@ -2792,11 +2826,19 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             const dim3 gp(static_cast<uint32_t>(std::min<uint64_t>(s->n_cu > 0 ? s->n_cu : 256, (npix + kProbeBlock - 1) / kProbeBlock)));
             if (lds_p <= kLdsCap) hipLaunchKernelGGL(rtw_cost_probe<true>, gp, dim3(kProbeBlock), lds_p, st, Q);
             else hipLaunchKernelGGL(rtw_cost_probe<false>, gp, dim3(kProbeBlock), 0, st, Q);
+            // hot pixels only if the probe can reach hot_segs: with the default cap of 8
+            // segments per sample (16 per pixel) and hot_segs 20 it cannot, and the two
+            // per-pixel launches are skipped. Enabling them measured slower everywhere
+            // (RTW_HOT_SEGS=16: N=1 +1.1 %, N=4 rank 60.7 -> 68.5 ms; a deeper probe,
+            // RTW_PROBE_CAP=16/24/50: N=1 +0.3/+2.2/+2.7 %, N=4 68-69 ms;
+            // profiles/r05_misc/knobs_probe_hot_REJECTED.log): long pixels promoted to
+            // the front start together and queue for the drains.
+            const bool hot = P.hot_segs <= kProbeSamples * P.probe_cap;
             hipLaunchKernelGGL(rtw_cost_bucket, gt, dim3(kBlock), 0, st, P);
-            hipLaunchKernelGGL(rtw_cost_hot_bucket, g1, dim3(kBlock), 0, st, P);
+            if (hot) hipLaunchKernelGGL(rtw_cost_hot_bucket, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_scan, dim3(1), dim3(64), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_place, gt, dim3(kBlock), 0, st, P);
-            hipLaunchKernelGGL(rtw_cost_hot_place, g1, dim3(kBlock), 0, st, P);
+            if (hot) hipLaunchKernelGGL(rtw_cost_hot_place, g1, dim3(kBlock), 0, st, P);
             hipLaunchKernelGGL(rtw_cost_scatter, gw, dim3(kBlock), 0, st, P);
             HIPCHECK(hipGetLastError());
         }
