@@ -27,7 +27,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra 
 LIB_SRCS := $(sort $(wildcard $(SRC)/*.hip $(SRC)/*.h $(SRC)/host/*.cpp $(SRC)/host/*.h)) include/rtw_capi.h
 BUILD_ID := $(shell cat $(LIB_SRCS) | sha256sum | cut -c1-12)-$(shell echo '$(ARCH) $(HIPFLAGS)' | sha256sum | cut -c1-4)
 
-all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check $(OUT)/try_check $(OUT)/defer_model
+all: $(OUT)/librtw.so $(OUT)/rtw_cli oracle $(OUT)/accel_check $(OUT)/next01_check $(OUT)/try_check $(OUT)/karg_check.ok
 
 $(OUT)/rtw_render.o: $(SRC)/rtw_render.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
 	@mkdir -p $(OUT)
@@ -59,10 +59,6 @@ $(OUT)/try_check: tools/try_check.cpp $(SRC)/rtw_numeric.h $(OUT)/librtw.so
 # test infrastructure: host self-check of the BVH walk (tests/test_accel.py)
 $(OUT)/accel_check: tools/accel_check.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
 	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/accel_check.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
-
-# developer tool: host model of the lane-compacted leaf pass (RTW_DEFER_LEAVES builds)
-$(OUT)/defer_model: tools/defer_model.cpp $(OUT)/rtw_accel_build.o $(OUT)/librtw.so
-	$(CXX) $(CXXFLAGS) -I$(SRC) -o $@ tools/defer_model.cpp $(OUT)/rtw_accel_build.o -L$(OUT) -lrtw -Wl,-rpath,'$$ORIGIN'
 
 # rewritten only when the id changes (so an unchanged tree rebuilds nothing)
 $(OUT)/rtw_build_id.h: FORCE
@@ -96,9 +92,24 @@ $(OUT)/rtw_host_stamps.o: $(SRC)/host/rtw_host.cpp include/rtw_capi.h $(SRC)/hos
 $(OUT)/librtw_stamps.so: $(OUT)/rtw_render_stamps.o $(OUT)/rtw_fast.o $(OUT)/rtw_group.o $(OUT)/rtw_host_stamps.o $(OUT)/rtw_accel_build.o
 	$(HIPCC) $(ARCHFLAGS) -shared -fPIC -o $@ $^ -Wl,-soname,librtw_stamps.so -lpthread
 
-asm: $(SRC)/rtw_render.hip
+RENDER_DEPS := $(SRC)/rtw_render.hip $(SRC)/rtw_fast.h $(SRC)/rtw_accel.h $(SRC)/rtw_numeric.h include/rtw_capi.h $(SRC)/host/rtw_host.h $(SRC)/host/rtw_internal.h
+asm: build/rtw_render.s
+build/rtw_render.s: $(RENDER_DEPS)
 	@mkdir -p build
-	$(HIPCC) --offload-arch=$(firstword $(ARCH)) $(HIPFLAGS_1) --cuda-device-only -S -o build/rtw_render.s $<
+	$(HIPCC) --offload-arch=$(firstword $(ARCH)) $(HIPFLAGS_1) --cuda-device-only -S -o $@ $<
+
+# Build-time guard of KP()/CamRef: every function of the render
+# file that reads KParams through the kernarg segment must be a lone-KParams kernel
+# without calls (tools/check_karg.py). Part of `all`: an outlined helper fails the build.
+$(OUT)/karg_check.ok: build/rtw_render.s tools/check_karg.py
+	@mkdir -p $(OUT)
+	python3 tools/check_karg.py build/rtw_render.s
+	@touch $@
+# its self-test: write_pixel deliberately noinline (RTW_KARG_SELFTEST) must be rejected
+karg-selftest: $(RENDER_DEPS) tools/check_karg.py
+	@mkdir -p build
+	$(HIPCC) --offload-arch=$(firstword $(ARCH)) $(HIPFLAGS_1) -DRTW_KARG_SELFTEST --cuda-device-only -S -o build/rtw_render_selftest.s $<
+	python3 tools/check_karg.py build/rtw_render_selftest.s --expect-fail
 
 # A/B variant of the library (tools/libab.py): make ablib NAME=x EXTRA=-DFOO -> ab/x/librtw.so
 ablib:
@@ -108,5 +119,5 @@ clean:
 	rm -rf $(OUT) build
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle asm clean stamps ablib FORCE
+.PHONY: all oracle asm clean stamps ablib karg-selftest FORCE
 FORCE:

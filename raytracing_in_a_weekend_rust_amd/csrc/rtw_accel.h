@@ -315,12 +315,6 @@ struct ArrayScratch {
         bad |= keep && !ok ? 1u : 0u;
     }
     RTW_HD uint32_t cand_at(uint32_t j) const { return e[kScratch - 1u - j]; }
-    // kDefer walks: every hit leaf child joins the list unfiltered (host: no flush)
-    template <typename F4>
-    RTW_HD void add_pending(uint64_t refs, uint32_t lmask, const F4 *, const WalkRay &, float &) {
-        for (uint32_t j = 0; j < 4u; ++j)
-            if ((lmask >> j) & 1u) add_cand(static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, true);
-    }
 };
 #if defined(__HIPCC__)
 // LdsScratch (device): a per-lane LDS column, slot k at col[k * stride] (u16);
@@ -354,47 +348,6 @@ struct LdsScratch {
         bad |= keep && !ok ? 1u : 0u;
     }
     __device__ uint32_t cand_at(uint32_t j) const { return base[(kScratch - 1u - j) * stride]; }
-    // kDefer walks: entries [0, nk) of the list are filtered survivors, [nk, nc) are
-    // listed unfiltered. flush_local filters the lane's own pending entries in place
-    // (the leaf_test filter and sure-hit cut) when the next node's leaves would not fit.
-    uint32_t nk = 0;
-    template <typename F4>
-    __device__ void flush_local(const F4 *__restrict__ leaves, const WalkRay &r, float &U) {
-        uint32_t w = nk;
-        for (uint32_t i = nk; i < nc; ++i) {
-            const uint32_t k = base[(kScratch - 1u - i) * stride];
-            const F4 S = leaves[2 * k];
-            const float d2 = leaves[2 * k + 1].x;
-            const float ocx = r.ox - S.x, ocy = r.oy - S.y, ocz = r.oz - S.z;
-            const float hb = fmaf(ocx, r.ex, fmaf(ocy, r.ey, ocz * r.ez));
-            const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-            const float disc = fmaf(hb, hb, -cc);
-            base[(kScratch - 1u - w) * stride] = static_cast<uint16_t>(k);
-            w += !(disc < r.negG) ? 1u : 0u;
-            const float sd = sqrt32(disc);
-            const float slo = sqrt32(fmaxf(disc - d2 + 2.f * r.negG, 0.f)) - hb;
-            const float slack = 1.953125e-3f * (fabsf(hb) + sd);
-            const bool sure = disc > d2 - 2.f * r.negG && slo - slack > r.tmin * 1.001f;
-            U = fminf(U, sure ? sd - hb + slack : U);
-        }
-        const uint32_t d = nc - w;  // entries dropped: the list end moves back up
-        cand = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(cand) + d * 2u * stride);
-        lim = reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(lim) + d * 2u * stride);
-        nc = w, nk = w;
-    }
-    // the node's hit leaf children join the list unfiltered, four branch-free
-    // appends (an unkept slot is overwritten by the next)
-    template <typename F4>
-    __device__ void add_pending(uint64_t refs, uint32_t lmask, const F4 *__restrict__ leaves, const WalkRay &r,
-                                float &U) {
-        const uint32_t c = static_cast<uint32_t>(__builtin_popcount(lmask));
-        if (c != 0u && (nc + c > kMaxCand ||
-                        !(reinterpret_cast<char *>(top) + (c - 1u) * 2u * stride < reinterpret_cast<char *>(lim))))
-            flush_local(leaves, r, U);
-#pragma unroll
-        for (uint32_t j = 0; j < 4u; ++j)
-            add_cand(static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, __builtin_amdgcn_ubfe(lmask, j, 1u) != 0u);
-    }
 };
 #endif
 
@@ -405,11 +358,10 @@ struct LdsScratch {
 // the running cut; the caller seeds it from the "always" spheres. Returns false
 // on candidate-list or stack overflow (caller brute-forces). `visits` counts
 // loop iterations (node visits).
-// kDefer (the lane-compacted leaf pass): hit leaf children are
-// not tested here but appended unfiltered to the candidate list (stk.add_pending);
-// the caller filters them afterwards, wave-wide and compacted. U then shrinks only
-// by the always-spheres' hits.
-template <bool kDefer = false, typename F4, typename Scratch>
+// (The lane-compacted leaf pass -- hit leaf children listed unfiltered and filtered
+// wave-wide after the walk -- measured +53 % and was removed in round 6:
+// profiles/r05_misc/ab_compacted_leaf_pass_REJECTED.log, git history before it.)
+template <typename F4, typename Scratch>
 RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, const WalkRay &r,
                  float &U, uint32_t &visits, Scratch &stk) {
     const uint32_t sx = r.neg & 1u, sy = (r.neg >> 1) & 1u, sz = r.neg >> 2;
@@ -440,14 +392,10 @@ RTW_HD bool walk(const F4 *__restrict__ nodes, const F4 *__restrict__ leaves, co
         uint32_t lmask = hit & (masks >> 4);
         const uint32_t inner = hit & ~lmask & 15u;
         const uint64_t refs = (static_cast<uint64_t>(r23) << 32) | r01;
-        if constexpr (kDefer) {
-            stk.add_pending(refs, lmask, leaves, r, U);
-        } else {
-            while (lmask) {
-                const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
-                lmask &= lmask - 1u;
-                leaf_test(leaves, static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, r, U, stk);
-            }
+        while (lmask) {
+            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
+            lmask &= lmask - 1u;
+            leaf_test(leaves, static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, r, U, stk);
         }
         // hit inner children onto the stack far to near (branch-free puts), then
         // continue with the top = the nearest

@@ -416,16 +416,8 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
 // sum (3 x f64 columns), the BVH walk scratch (kScratch x u16 columns) and the
 // speculative draws' RNG state (one 16 B column).
-// RTW_DEFER_LEAVES (A/B build, the lane-compacted leaf pass): + a wave queue of
-// kMaxCand u16 entries per lane for the compacted filter pass (bvh_hit kDefer).
-#ifdef RTW_DEFER_LEAVES
-constexpr bool kDeferLeaves = true;
-#else
-constexpr bool kDeferLeaves = false;
-#endif
 __host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
-    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t) + 16 +
-                                           (kDeferLeaves ? rtw_accel::kMaxCand * sizeof(uint16_t) : 0));
+    return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t) + 16);
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -454,7 +446,10 @@ __device__ __forceinline__ kchar *karg_base() {
     const uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
     uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
     uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-    asm volatile("" : "+s"(lo), "+s"(hi));
+    // the comment tags every expansion for the build-time guard (tools/check_karg.py,
+    // `make karg-check`): the function holding it must be a lone-KParams kernel that
+    // makes no call -- an outlined helper would read some other argument block
+    asm volatile("; rtw-karg kparams=%2" : "+s"(lo), "+s"(hi) : "n"(sizeof(KParams)));
     return reinterpret_cast<kchar *>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 #define KP(f) (*reinterpret_cast<const __attribute__((address_space(4))) decltype(KParams::f) *>(karg_base() + offsetof(KParams, f)))
@@ -910,7 +905,14 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
     return false;
 }
 
-__device__ __forceinline__ void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
+// RTW_KARG_SELFTEST (`make karg-selftest` only, never a library): write_pixel outlined,
+// so the karg guard must reject the build
+#ifdef RTW_KARG_SELFTEST
+#define RTW_KARG_HELPER __attribute__((noinline))
+#else
+#define RTW_KARG_HELPER __forceinline__
+#endif
+__device__ RTW_KARG_HELPER void write_pixel(const KParams &P, uint32_t x, uint32_t lr,
                                             const PixelState &ps, bool count = true) {
     if (count && KP(pixels_done)) atomicAdd(KP(pixels_done), 1u);
     const double nf = static_cast<double>(KP(n_off));
@@ -1015,16 +1017,11 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
 // exact candidates, the cut check; anything unproven falls back to the scan.
 // kStride: the LDS scratch column stride (the workgroup size; a constant, so the
 // walk's pointer steps are immediates and hold no register)
-// kDefer (RTW_DEFER_LEAVES builds, LDS scratch only): the walk lists its hit leaf
-// children unfiltered (rtw_accel.h walk<true>) and the wave filters all of them in
-// one compacted pass -- lane t takes entry t, t + A, ... of the wave's list (A =
-// walking lanes) and reads its owner's ray by ds_bpermute -- instead of a trip per
-// leaf of the busiest lane at every node. wq: the wave's queue (kMaxCand u16 per lane).
-template <bool kLdsStack = false, uint32_t kStride = 0, bool kDefer = false>
+template <bool kLdsStack = false, uint32_t kStride = 0>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
-                                       double *sa_out = nullptr, uint16_t *wq = nullptr) {
+                                       double *sa_out = nullptr) {
     const double4 *__restrict__ sph = sv.sph;
     const float4 *__restrict__ nodes = sv.nodes;
     const float4 *__restrict__ leaves = sv.leaves;
@@ -1057,56 +1054,9 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
                 // after it: every wave that walks with kLdsStack is a cursor wave at that
                 // point (a priority wave that joins the cursor runs as one).
                 if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(kWalkPrio);
-                const bool walked = rtw_accel::walk<kDefer>(nodes, leaves, wr, U, tl.visits, ws);
+                const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
                 if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
                 STAMP(2);  // 2: BVH walk
-                if constexpr (kDefer) {
-                    static_assert(!kDefer || kLdsStack, "the compacted pass needs the LDS scratch");
-                    const uint32_t lane = threadIdx.x & 63u;
-                    const uint32_t nk = ws.nk;                      // filtered by flush_local
-                    const uint32_t n = walked ? ws.nc - nk : 0u;  // pending, nk + n <= kMaxCand
-                    auto below = [](uint64_t b) {
-                        return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
-                    };
-                    const uint64_t b0 = __ballot(n & 1u), b1 = __ballot(n & 2u), b2 = __ballot(n & 4u),
-                                   b3 = __ballot(n & 8u);
-                    const uint32_t P0 = below(b0) + 2u * below(b1) + 4u * below(b2) + 8u * below(b3);
-                    const uint32_t T = static_cast<uint32_t>(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2) +
-                                                             8 * __popcll(b3));
-                    for (uint32_t i = 0; i < n; ++i) wq[P0 + i] = static_cast<uint16_t>(lane | ((nk + i) << 6));
-                    __builtin_amdgcn_wave_barrier();
-                    const uint64_t ex = __ballot(1);
-                    const uint32_t A = static_cast<uint32_t>(__popcll(ex)), rank = below(ex);
-                    const uint16_t *wcol = scol - lane;  // this wave's lane-0 column
-                    for (uint32_t b = 0; b < T; b += A) {  // wave-uniform trips
-                        const uint32_t e = b + rank;
-                        const bool valid = e < T;
-                        const uint32_t ent = valid ? wq[e] : lane;
-                        const int o = static_cast<int>(ent & 63u);
-                        const float rox = __shfl(wr.ox, o), roy = __shfl(wr.oy, o), roz = __shfl(wr.oz, o);
-                        const float rex = __shfl(wr.ex, o), rey = __shfl(wr.ey, o), rez = __shfl(wr.ez, o);
-                        const float rng = __shfl(wr.negG, o);
-                        if (valid) {
-                            const uint32_t k = wcol[static_cast<uint32_t>(o) + (rtw_accel::kScratch - 1u - (ent >> 6)) * kStride];
-                            const float4 S = leaves[2 * k];
-                            const float ocx = rox - S.x, ocy = roy - S.y, ocz = roz - S.z;
-                            const float hb = fmaf(ocx, rex, fmaf(ocy, rey, ocz * rez));
-                            const float cc = fmaf(ocx, ocx, fmaf(ocy, ocy, fmaf(ocz, ocz, -S.w)));
-                            if (!(fmaf(hb, hb, -cc) < rng)) wq[e] = static_cast<uint16_t>(ent | 0x8000u);
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    // the owner keeps its survivors, in list order (slot w <= i: no overwrite
-                    // of an entry still to be read)
-                    uint32_t w = nk;
-                    for (uint32_t i = 0; i < n; ++i) {
-                        const uint32_t keep = static_cast<uint32_t>(wq[P0 + i]) >> 15;
-                        scol[(rtw_accel::kScratch - 1u - w) * kStride] = static_cast<uint16_t>(ws.cand_at(nk + i));
-                        w += keep;
-                    }
-                    if (walked) ws.nc = w;
-                }
                 if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
                     ++tl.ntest;
@@ -1750,9 +1700,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     double *acc = reinterpret_cast<double *>(lds_sph) + P.lane_lds_off / 8u + threadIdx.x;
     uint16_t *lane_stk = reinterpret_cast<uint16_t *>(acc - threadIdx.x + 3u * kThreads);
     uint4 *spec_lds = reinterpret_cast<uint4 *>(lane_stk + rtw_accel::kScratch * kThreads) + threadIdx.x;
-    // RTW_DEFER_LEAVES builds: this wave's queue for the compacted leaf pass
-    uint16_t *defer_q = reinterpret_cast<uint16_t *>(spec_lds - threadIdx.x + kThreads) +
-                        (threadIdx.x & ~63u) * rtw_accel::kMaxCand;
     const double4 *sph = sv.sph;
     Tally tl;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1768,8 +1715,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true, kThreads, kDeferLeaves>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp,
-                                                         lane_stk + threadIdx.x, &seg_sa, defer_q);
+            return bvh_hit<true, kThreads>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp,
+                                           lane_stk + threadIdx.x, &seg_sa);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
