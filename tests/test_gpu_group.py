@@ -211,5 +211,11 @@ def test_group_distinct_gpus(devices, kw, gather):
     assert torch.cuda.current_device() == 0
     total, per, info = g.stats()
     g.close()
-    assert info["gather"] in (gather, "copy") and (info["gather"] == gather or info["fallback"] != "none")
+    if gather == "rccl" and rtw.rccl_available()[0]:
+        # RCCL is loadable here: a fallback would hide an RCCL regression
+        assert info["gather"] == "rccl" and info["fallback"] == "none", info
+    elif gather == "rccl":
+        assert info["gather"] == "copy" and info["fallback"] != "none", info
+    else:
+        assert info["gather"] == "copy", info
     assert np.array_equal(out.cpu().numpy(), ref) and total.segments == seg
