@@ -269,7 +269,8 @@ int rtw_session_diag(rtw_session *s, uint32_t *out, uint64_t cap);
  * says why (rtw_group_info.fallback, rtw_group_note); only RTW_GROUP_RCCL_ALWAYS
  * makes that an error. Renders are blocking: on return the image is complete in
  * out_rgb_device. The root device's first write to out_rgb_device is ordered
- * after the work already queued on that device's null stream. Every rtw_group_*
+ * after the work already queued on that device's null stream (or on the caller's
+ * stream: rtw_group_render_on). Every rtw_group_*
  * call restores the caller's current HIP device. Bit-identical to a one-device
  * render. */
 typedef struct rtw_group rtw_group;
@@ -303,6 +304,14 @@ int rtw_group_render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt,
 /* f32 fast mode; out_rgb_device: H*W*3 f32 on the root device. */
 int rtw_group_render_fast(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt,
                           rtw_u128 seed, float *out_rgb_device);
+/* The same, ordered after the work queued on caller_stream (a hipStream_t of the root
+ * device; NULL = its null stream, what rtw_group_render does) instead of the null
+ * stream: a caller inside torch.cuda.stream(s), or on a per-thread default stream,
+ * passes that stream. Still blocking. */
+int rtw_group_render_on(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                        double *out_rgb_device, void *caller_stream);
+int rtw_group_render_fast_on(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt,
+                             rtw_u128 seed, float *out_rgb_device, void *caller_stream);
 /* Last render: total (counters summed, times the slowest entry's; nullable),
  * per_entry[0..n_entries) (nullable; RTW_E_CAPACITY if cap < n_entries) and info
  * (nullable). */

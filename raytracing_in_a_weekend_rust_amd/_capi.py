@@ -138,6 +138,9 @@ SIGNATURES = {
                                       C.c_uint32]),
     "rtw_group_render": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
     "rtw_group_render_fast": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p]),
+    "rtw_group_render_on": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p, C.c_void_p]),
+    "rtw_group_render_fast_on": (C.c_int, [C.c_void_p, _P(Camera), C.c_uint32, U128, C.c_void_p,
+                                           C.c_void_p]),
     "rtw_group_stats": (C.c_int, [C.c_void_p, _P(Stats), _P(Stats), C.c_uint32, _P(GroupInfo)]),
     "rtw_group_note": (C.c_char_p, [C.c_void_p]),
     "rtw_rccl_available": (C.c_int, [C.c_char_p, C.c_size_t]),

@@ -389,15 +389,17 @@ class Group:
     def set_scene(self, sph, n_sph, mats, n_mats):
         check(lib.rtw_group_set_scene(self.h, sph, n_sph, mats, n_mats))
 
-    def render(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int):
-        """The whole image into an H x W x 3 f64 buffer on the root device."""
-        check(lib.rtw_group_render(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
-                                   C.c_void_p(out_dev_ptr)))
+    def render(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int, stream: int = 0):
+        """The whole image into an H x W x 3 f64 buffer on the root device, ordered after
+        the work queued on `stream` (a hipStream_t handle of the root device, e.g.
+        torch.cuda.current_stream().cuda_stream; 0 = the null stream)."""
+        check(lib.rtw_group_render_on(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
+                                      C.c_void_p(out_dev_ptr), C.c_void_p(stream or None)))
 
-    def render_fast(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int):
-        """f32 fast mode into an H x W x 3 f32 buffer on the root device."""
-        check(lib.rtw_group_render_fast(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
-                                        C.c_void_p(out_dev_ptr)))
+    def render_fast(self, cam: capi.Camera, samples_sqrt: int, seed: int, out_dev_ptr: int, stream: int = 0):
+        """f32 fast mode into an H x W x 3 f32 buffer on the root device (`stream` as render)."""
+        check(lib.rtw_group_render_fast_on(self.h, C.byref(cam), samples_sqrt, capi.U128.of(seed),
+                                           C.c_void_p(out_dev_ptr), C.c_void_p(stream or None)))
 
     def stats(self):
         """(total Stats, [per-entry Stats], info dict) of the last render."""

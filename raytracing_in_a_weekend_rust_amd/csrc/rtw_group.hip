@@ -269,7 +269,8 @@ void create(const int *devices, uint32_t n_devices, uint32_t flags, rtw_group **
 }
 
 template <typename T>
-void render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed, bool fast, T *out) {
+void render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed, bool fast, T *out,
+            hipStream_t caller) {
     const auto t0 = std::chrono::steady_clock::now();
     if (!cam || !out) throw rtw::Error(RTW_E_ARG, "null argument");
     const uint32_t H = cam->img_height, W = cam->img_width;
@@ -285,11 +286,12 @@ void render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128
     Entry &root = g->e[0];
     if (gather != RTW_GATHER_NONE) grow(g->gathered, g->gathered_cap, n * tile_bytes, root.device);
     // The root stream is non-blocking, so order it after the work the caller already
-    // queued on the root device's null stream (torch's default stream), which may
-    // still read or write `out`: the root stream's first write to `out` (the one-entry
-    // render, or the un-permute) waits for it.
+    // queued on its stream on the root device (`caller`: NULL = the null stream, torch's
+    // default stream; rtw_group_render_on passes a torch.cuda.stream's or a per-thread
+    // stream), which may still read or write `out`: the root stream's first write to
+    // `out` (the one-entry render, or the un-permute) waits for it.
     hip_check(hipSetDevice(root.device), "hipSetDevice");
-    hip_check(hipEventRecord(g->caller, nullptr), "hipEventRecord (caller stream)");
+    hip_check(hipEventRecord(g->caller, caller), "hipEventRecord (caller stream)");
     hip_check(hipStreamWaitEvent(root.stream, g->caller, 0), "hipStreamWaitEvent");
 
     // 1. every entry's rows, enqueued on its own stream (asynchronous)
@@ -425,18 +427,30 @@ int rtw_group_set_scene(rtw_group *g, const rtw_sphere *spheres, uint32_t n_sphe
     RTW_GROUP_GUARD(for (auto &x : g->e) api_check(rtw_session_set_scene(x.sess, spheres, n_spheres, mats, n_mats)))
 }
 
-int rtw_group_render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
-                     double *out_rgb_device) {
+int rtw_group_render_on(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                        double *out_rgb_device, void *caller_stream) {
     if (!g) return rtw::set_error("null group"), RTW_E_ARG;
     std::lock_guard<std::mutex> lock(g->mu);
-    RTW_GROUP_GUARD(render<double>(g, cam, samples_sqrt, seed, false, out_rgb_device))
+    RTW_GROUP_GUARD(render<double>(g, cam, samples_sqrt, seed, false, out_rgb_device,
+                                   static_cast<hipStream_t>(caller_stream)))
+}
+
+int rtw_group_render_fast_on(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                             float *out_rgb_device, void *caller_stream) {
+    if (!g) return rtw::set_error("null group"), RTW_E_ARG;
+    std::lock_guard<std::mutex> lock(g->mu);
+    RTW_GROUP_GUARD(render<float>(g, cam, samples_sqrt, seed, true, out_rgb_device,
+                                  static_cast<hipStream_t>(caller_stream)))
+}
+
+int rtw_group_render(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
+                     double *out_rgb_device) {
+    return rtw_group_render_on(g, cam, samples_sqrt, seed, out_rgb_device, nullptr);
 }
 
 int rtw_group_render_fast(rtw_group *g, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u128 seed,
                           float *out_rgb_device) {
-    if (!g) return rtw::set_error("null group"), RTW_E_ARG;
-    std::lock_guard<std::mutex> lock(g->mu);
-    RTW_GROUP_GUARD(render<float>(g, cam, samples_sqrt, seed, true, out_rgb_device))
+    return rtw_group_render_fast_on(g, cam, samples_sqrt, seed, out_rgb_device, nullptr);
 }
 
 int rtw_group_stats(rtw_group *g, rtw_stats *total, rtw_stats *per_entry, uint32_t cap, rtw_group_info *info) {

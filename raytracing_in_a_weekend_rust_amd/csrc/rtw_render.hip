@@ -156,6 +156,9 @@ struct KParams {
     uint32_t drain_prio;        // draining waves' issue priority after the cursor phase (RTW_DRAIN_PRIO,
                                 // default 3; 0: unchanged)
     uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
+    uint32_t spread_q;          // > 0: hand-out ticket t < 64 q takes order position (t % 64) q + t / 64,
+                                // so a wave's 64 lanes get pixels from across the cost order
+                                // (RTW_SPREAD; 0: position t)
     uint32_t prepark;           // cost-ordered hand-out: a pixel whose probe traced >= prepark
                                 // segments is parked before its first sample (0: off)
     uint64_t seed_lo, seed_hi;
@@ -678,6 +681,13 @@ constexpr int kGather = RTW_TRY_GATHER;  // table columns loaded per trip of the
 __device__ __forceinline__ uint64_t unit_vec_round(const uint4 *__restrict__ tries, U128 s, U128 &st, double &ux,
                                                    double &uy, double &uz) {
     const uint32_t lane = __lane_id();
+#ifdef RTW_STAMPS  // diagnostic build: the whole-wave, wave-uniform-state assumption
+    if (__ballot(1) != ~0ull ||
+        static_cast<uint32_t>(s.lo) != static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s.lo))) ||
+        static_cast<uint32_t>(s.hi >> 32) !=
+            static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s.hi >> 32))))
+        __builtin_trap();
+#endif
     const uint4 *col = tries + lane;
     uint64_t lo = 0, hi = 0;
     for (uint32_t h = 0; h < 2; ++h) {
@@ -1405,16 +1415,21 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     ps.rng = U128{q.rng_lo, q.rng_hi};
     ps.k = q.k;
     ps.ar = q.ar, ps.ag = q.ag, ps.ab = q.ab;
-    const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
-    if (sub == 0) diag_event(P, static_cast<uint64_t>(P.n_rows) * P.W, pix, 2);
+    // (the pixel index is formed where the diagnostics use it: held from here to the
+    // end of the pixel, it was spilled to scratch)
+    if (sub == 0) diag_event(P, static_cast<uint64_t>(P.n_rows) * P.W, static_cast<uint64_t>(q.lr) * P.W + q.x, 2);
     // scenes of up to kCoopRegRec * kG spheres: the lane's pass-1 records live in
     // registers for the whole pixel (no LDS round trip on the serial chain)
     constexpr uint32_t kCoopRegRec = 8;
     const bool rec_in_regs = n <= kCoopRegRec * kG;
     float4 rr[kCoopRegRec];
     if (rec_in_regs) {
+        // the record addresses are formed per pixel from a laundered lane id: hoisted
+        // out of the drain loop, the compiler kept all eight through it and spilled them
+        uint32_t sl = sub;
+        asm volatile("" : "+v"(sl));
 #pragma unroll
-        for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sub + j * kG, n - 1u) << fsh];
+        for (uint32_t j = 0; j < kCoopRegRec; ++j) rr[j] = filt[min(sl + j * kG, n - 1u) << fsh];
     }
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
@@ -1467,12 +1482,17 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
         return best;
     };
     uint32_t s = 0, trapped = 0;
-    trace_samples<true, kG == 64>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    // the lane-parallel replay (trap_forward<true>, unit_vec_round) needs the whole wave
+    // on one path with one RNG state: only 64-lane groups take it
+    constexpr bool kWaveReplay = kG == 64;
+    static_assert(!kWaveReplay || kG == 64, "the trapped-path replay runs on whole waves only");
+    trace_samples<true, kWaveReplay>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
     if (sub == 0) tl.trap += trapped;
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
         uint32_t *diag = KP(diag);
         if (diag) {
+            const uint64_t pix = static_cast<uint64_t>(q.lr) * P.W + q.x;
             atomicAdd(diag + 2 * pix, s);
             __hip_atomic_store((gu32 *)(diag + 2 * pix + 1),
                                static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()), __ATOMIC_RELAXED,
@@ -1526,6 +1546,17 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t segs, uint32_t pixels) 
 // each and ran at one workgroup per CU); the walk stack lives in per-lane LDS
 // columns at P.lane_lds_off (kLds) instead of scratch memory.
 constexpr uint32_t kProbeBlock = 768;
+// SplitMix64's finaliser (Steele, Lea & Flood), for the probe's per-pixel xorshift state
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ U128 probe_state(uint64_t seed_lo, uint64_t seed_hi, uint64_t gpix) {
+    const uint64_t a = seed_lo + (gpix + 1ull) * 0x9e3779b97f4a7c15ull;
+    const U128 r{mix64(a), mix64(a ^ seed_hi ^ 0x6a09e667f3bcc909ull)};
+    return (r.lo | r.hi) ? r : U128{1ull, 0ull};  // xorshift's state must not be zero
+}
 template <bool kLds>
 __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
@@ -1550,7 +1581,10 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         const uint64_t i = static_cast<uint64_t>(lr) * P.W + x;
         const uint32_t wgt = min(sub, P.W - x) * min(sub, P.n_rows - lr);
         const PixelLoc pl(P, x, P.row_begin + lr * P.row_step);
-        U128 rng = P.seeds[i];  // a copy: the render starts from the same child
+        // the probe's own stream (a hash of the render seed and the global pixel index),
+        // not the pixel's RNG child: the estimate is as good, and the probe no longer
+        // waits for rtw_seed_pixels, which runs beside it on the session's second stream
+        U128 rng = probe_state(P.seed_lo, P.seed_hi, static_cast<uint64_t>(P.row_begin + lr * P.row_step) * P.W + x);
         uint32_t segs = 0;
         for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
             Path p;
@@ -1707,7 +1741,14 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     const uint64_t stride = P.spill_stride;
     // spill column of this lane for the whole launch: consecutive lanes of a wave
     // share L2 lines, and the live columns stay dense
-    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    // re-formed at each use from the workgroup id and the lane's thread id (laundered
+    // through an empty asm so it is not one 64-bit value held across the whole
+    // persistent loop: the compiler spilled it to scratch, round 5's private segment)
+    auto gid = [&]() -> uint64_t {
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return static_cast<uint64_t>(blockIdx.x) * kThreads + t;
+    };
     const bool heavy_wave = (threadIdx.x >> 6) < P.heavy_per_block;
 
     Stamps stp_unused, stp;  // stp: cursor-loop sections (RTW_STAMPS builds only)
@@ -1775,7 +1816,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+            cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid() & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
             if (sub == 0) atomicAdd(P.park_processed, 1u);
         }
         tl.seg += cseg;
@@ -1811,7 +1852,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     // rows bottom-up when P.order == 1, or row-major
                     const uint32_t *order_map = KP(order_map);
                     if (order_map) {
-                        pix = order_map[ticket];
+                        const uint64_t q = KP(spread_q);
+                        const uint64_t pos = ticket < 64u * q ? (ticket & 63u) * q + (ticket >> 6) : ticket;
+                        pix = order_map[pos];
                         lr = static_cast<uint32_t>(pix / P.W);
                         x = static_cast<uint32_t>(pix - static_cast<uint64_t>(lr) * P.W);
                     } else {
@@ -1950,7 +1993,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
                 if (kind != RTW_DIELECTRIC) {  // the bounce's attenuation row
                     if (ended) cr = M.a0 * 0., cg = M.a1 * 0., cb = M.a2 * 0.;  // att x black
-                    else p.stk.push(static_cast<uint32_t>(best), KP(spill), stride, gid);
+                    else p.stk.push(static_cast<uint32_t>(best), KP(spill), stride, gid());
 #ifdef RTW_WALK_DIAG
                     if (!ended && p.stk.n > kRegSlots) atomicAdd(&P.counters[18], 1ull);  // spill-level pushes
 #endif
@@ -1966,7 +2009,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 if (best >= 0 && KP(att_finite)) {  // black leaf: +-0, no fold (see trace_samples)
                     p.stk.clear();
                 } else {
-                    fold(sv.shd, p, KP(spill), gid, stride, cr, cg, cb);
+                    fold(sv.shd, p, KP(spill), gid(), stride, cr, cg, cb);
                     acc[0] = acc[0] + cr, acc[kThreads] = acc[kThreads] + cg, acc[2 * kThreads] = acc[2 * kThreads] + cb;
                 }
                 done = ++ps.k >= KP(n_off);
@@ -2178,7 +2221,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
+        cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid() & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
         if (sub == 0) atomicAdd(P.park_processed, 1u);
     }
     tl.seg += cseg;
@@ -2317,6 +2360,10 @@ struct rtw_session {
     bool last_fast = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_k0 = nullptr, ev_k1 = nullptr;  // around the main kernel (rtw_stats.main_kernel_ms)
+    // the seed kernel runs on `aux` beside the cost probe (fork / join events on the
+    // render's stream)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool main_ev = false;                         // the last render recorded them
     uint32_t *d_err = nullptr;  // latched count of incomplete renders (rtw_latch_check)
     hipStream_t last_stream = nullptr;
@@ -2746,13 +2793,25 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // per-pixel seeds (a separate launch: measured 0.7 ms faster than deriving
         // them inside the LDS-heavy cost probe)
         const uint64_t seed_threads = static_cast<uint64_t>(P.n_rows) * ((P.W + kSeedRun - 1) / kSeedRun);
-        hipLaunchKernelGGL(rtw_seed_pixels, dim3(static_cast<uint32_t>((seed_threads + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, st, P);
-        HIPCHECK(hipGetLastError());
+        const dim3 g_seed(static_cast<uint32_t>((seed_threads + kBlock - 1) / kBlock));
         // hand-out order: RTW_ORDER=2 (default with a BVH) by estimated cost, 1 rows
         // bottom-up, 0 row-major
         P.order_map = nullptr;
-        if (P.order == 2 && mode == kBvh && P.max_depth > 0) {
+        const bool probe = P.order == 2 && mode == kBvh && P.max_depth > 0;
+        // With the probe, the seeds are computed on the session's second stream beside
+        // it (the probe draws from its own per-pixel stream) and joined before the
+        // persistent kernel: the seed kernel's 0.14 ms leaves the frame's serial part.
+        if (probe) {
+            HIPCHECK(hipEventRecord(s->ev_fork, st));
+            HIPCHECK(hipStreamWaitEvent(s->aux, s->ev_fork, 0));
+            hipLaunchKernelGGL(rtw_seed_pixels, g_seed, dim3(kBlock), 0, s->aux, P);
+            HIPCHECK(hipGetLastError());
+            HIPCHECK(hipEventRecord(s->ev_join, s->aux));
+        } else {
+            hipLaunchKernelGGL(rtw_seed_pixels, g_seed, dim3(kBlock), 0, st, P);
+            HIPCHECK(hipGetLastError());
+        }
+        if (probe) {
             P.cost = s->d_cost, P.cost_hist = s->d_cost_hist, P.order_map = s->d_order, P.pcost = s->d_pcost;
             const dim3 g1(static_cast<uint32_t>((npix + kBlock - 1) / kBlock));
             const TileGrid tg(P);
@@ -2760,7 +2819,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
             const dim3 gw((tg.count() * 64u + kBlock - 1) / kBlock);  // one wave per tile
             HIPCHECK(hipMemsetAsync(s->d_cost_hist, 0, kCostBuckets * sizeof(uint32_t), st));
             HIPCHECK(hipMemsetAsync(s->d_cost, 0, 2 * static_cast<size_t>(tg.count()) * sizeof(uint32_t), st));
-            P.probe_sub = 1;
+            // full images below 400 samples per pixel probe one pixel per 2x2 block: the
+            // probe's ~0.75 ms does not shrink with the samples while the frame does
+            // (config 3, s=10: 26.89 -> 26.58 ms, profiles/r06_misc/); small shards keep
+            // every pixel's probe (their pre-parking reads it), and so do s >= 20 frames
+            // (neutral there, profiles/r02_misc/knob_probe_sub.log)
+            const double fill_est = static_cast<double>(npix) / (static_cast<double>(s->n_cu > 0 ? s->n_cu : 256) * kPBlock);
+            P.probe_sub = fill_est >= 1.5 && P.n_off < 400u ? 2u : 1u;
             if (const char *e = kn.get("RTW_PROBE_SUB")) P.probe_sub = static_cast<uint32_t>(std::max(1, std::atoi(e)));
             P.probe_cap = kProbeCap, P.hot_segs = kHotSegs;
             if (const char *e = kn.get("RTW_PROBE_CAP")) P.probe_cap = static_cast<uint32_t>(std::max(1, std::atoi(e)));
@@ -2887,9 +2952,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
         if (const char *e = kn.get("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (const char *e = kn.get("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
+        P.spread_q = 0;
+        if (const char *e = kn.get("RTW_SPREAD"))
+            if (std::atoi(e) != 0 && P.order_map) P.spread_q = static_cast<uint32_t>(npix / 64u);
         if (const char *e = kn.get("RTW_DRAIN_PRIO")) P.drain_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (P.rate_x == 0) P.rate_k = 0xffffffffu;  // rate-based parking off
         HIPCHECK(hipMemsetAsync(s->d_park_flag, 0, npix * sizeof(uint32_t), st));
+        if (probe) HIPCHECK(hipStreamWaitEvent(st, s->ev_join, 0));  // the seeds are written
         void *args[] = {&P};
         HIPCHECK(hipEventRecord(s->ev_k0, st));
         HIPCHECK(hipLaunchKernel(fn, dim3(grid_p), dim3(pblock), args, lds, st));
@@ -3086,6 +3155,9 @@ void create_session(int device, rtw_session **out) {
         HIPCHECK(hipEventCreate(&s->ev1));
         HIPCHECK(hipEventCreate(&s->ev_k0));
         HIPCHECK(hipEventCreate(&s->ev_k1));
+        HIPCHECK(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+        HIPCHECK(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
         HIPCHECK(hipMalloc(&s->d_counters, kCounters * sizeof(unsigned long long)));
         HIPCHECK(hipMalloc(&s->d_park_ctl, 8 * sizeof(uint32_t)));
         HIPCHECK(hipMalloc(&s->d_err, sizeof(uint32_t)));
@@ -3255,6 +3327,9 @@ int rtw_session_destroy(rtw_session *s) {
     if (s->ev_k0) (void)hipEventDestroy(s->ev_k0);
     if (s->ev_k1) (void)hipEventDestroy(s->ev_k1);
     if (s->own) (void)hipStreamDestroy(s->own);
+    if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+    if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+    if (s->aux) (void)hipStreamDestroy(s->aux);
     delete s;
     return RTW_OK;
 }

@@ -141,6 +141,27 @@ def test_group_orders_after_callers_null_stream():
         g.close()
 
 
+def test_group_orders_after_callers_stream():
+    """Inside torch.cuda.stream(s) the caller's pending work is on s, not on the null
+    stream: render(..., stream=s) orders the group's first write to `out` after it
+    (ADVICE r05). A spin then a fill of `out` on s precede the render."""
+    cam, sph, n, mt, nm = scene()
+    ref, _ = orc.render(cam.raw, sph, n, mt, nm, 2, SEED)
+    side = torch.cuda.Stream(device="cuda:0")
+    for devices in ([0], [0, 0]):
+        g = rtw.Group(devices)
+        g.set_scene(sph, n, mt, nm)
+        out = torch.zeros((27, 48, 3), dtype=torch.float64, device="cuda:0")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(200_000_000)  # ~0.1 s of spinning on the caller's stream
+            out.fill_(-7.0)
+            g.render(cam.raw, 2, SEED, out.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref), devices
+        g.close()
+
+
 _FALLBACK_CHILD = r"""
 import sys, numpy as np, torch
 import raytracing_in_a_weekend_rust_amd as rtw
