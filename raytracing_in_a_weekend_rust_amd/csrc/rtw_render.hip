@@ -79,6 +79,11 @@ constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 s
                                             // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
+#ifndef RTW_ENDGAME_POLL
+#define RTW_ENDGAME_POLL 16
+#endif
+constexpr uint32_t kEndgamePoll = RTW_ENDGAME_POLL;  // cursor iterations per endgame poll (a power of 2)
+static_assert((kEndgamePoll & (kEndgamePoll - 1u)) == 0u, "kEndgamePoll: a power of two");
 
 // Scene::hit strategies (one kernel instantiation each)
 constexpr int kScanF64 = 0;  // the reference's scan, f64 only
@@ -1825,6 +1830,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         bool need = true;  // lane holds no pixel
         bool dry = false;  // wave-uniform: the cursor ran dry
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
+        uint32_t wave_it = 0;  // wave-uniform: iterations of this wave's cursor loop
         uint32_t x = 0, lr = 0, pseg = 0;
         bool spec = false;  // spec_lds holds the state the lane's next unit vector draws from
         uint64_t pix = 0;
@@ -1891,11 +1897,15 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
             }
             dry = dry || __any(dry_now);  // wave-uniform
+            ++wave_it;
             // endgame: once the cursor is dry and at most P.endgame pixels of the shard
             // are unfinished (about one per drain group), every lane parks its pixel
             // at its next sample boundary -- the last chains then run on a whole wave
-            // each (a segment every ~2 us) instead of one lane of a wave (~16 us)
-            if (dry && !endgame && P.endgame)
+            // each (a segment every ~2 us) instead of one lane of a wave (~16 us).
+            // The count is polled every kEndgamePoll-th iteration: the device-scope load
+            // is waited on at once, and in a small shard (dry from the first fill) every
+            // cursor wave paid that round trip in every iteration
+            if (dry && !endgame && P.endgame && (wave_it & (kEndgamePoll - 1u)) == 0u)
                 endgame = static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(ld_rlx(KP(pixels_done)))) + P.endgame >= npix;
 
             if (__all(need)) {
