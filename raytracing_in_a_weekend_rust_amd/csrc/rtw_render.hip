@@ -861,11 +861,17 @@ __device__ __forceinline__ void fold(const ShadeRec *__restrict__ shd, Path &p, 
 // With kTrap (drain groups: one path per group, so the branch is uniform) a
 // path trapped inside a sphere is fast-forwarded to its depth cap (trap_forward);
 // `trapped` counts the segments skipped that way.
-template <bool kTrap = false, bool kWave = false, class HitFn>
+// tir_run (64-lane drain groups): called after a total internal reflection inside S
+// whose great-circle forward already failed; it may trace the run's next bounces in
+// place (returning how many), leaving the path exactly as the generic loop would.
+struct NoTirRun {
+    __device__ uint32_t operator()(Path &, int) const { return 0u; }
+};
+template <bool kTrap = false, bool kWave = false, class HitFn, class TirRun = NoTirRun>
 __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView &sv,
                                               uint32_t x, uint32_t y, uint16_t *spill, uint64_t col,
                                               PixelState &ps, uint32_t budget, uint32_t &seg, Stamps &stp,
-                                              HitFn &&hit, uint32_t *trapped = nullptr) {
+                                              HitFn &&hit, uint32_t *trapped = nullptr, TirRun &&tir_run = TirRun{}) {
     const uint32_t n_off = P.n_off;
     if (P.max_depth == 0) {  // every sample is black (no Scene::hit call)
         ps.k = n_off;
@@ -904,6 +910,9 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
                 if (!k && th.tir) tir_no = best;
                 if (k) seg += k, *trapped += k, done = true;  // (lr, lg, lb) = 0: the black leaf
             }
+            // the run goes on: its next bounces by the lean loop (they draw nothing and
+            // their forward tests would fail again)
+            if (!done && th.tir && best == tir_no) seg += tir_run(p, best);
         }
         STAMP(3);  // 3: trapped-path check (kTrap)
         if (done) {
@@ -1392,6 +1401,88 @@ __device__ __forceinline__ bool inside_hit_group(const double4 *__restrict__ sph
     return true;
 }
 
+// A run of total internal reflections inside sphere S, traced by a whole drain wave
+// (the long serial chains of the strong split: 66 % of row 308's segments are such
+// bounces inside the big glass sphere, 4.2 per run, profiles/r05_misc/
+// trace_pixel_567_308.log). The path has just reflected totally inside S and S's
+// great-circle forward failed, so the generic loop would take, bounce after bounce,
+// the inside cut (S's far root beside its list, inside_hit_group), the dielectric
+// scatter's reflection (shade) and skip the forward test. Here S's record, its
+// shading row and each lane's list entry stay in registers for the run, and a
+// bounce is exactly those operations, in the same order on the same values:
+// a = |d|^2, inside_hit_group's roots and (t, index) minimum, the hit point,
+// (p - c) / r, front, unit(d), cos_t, tir_exceeds, the reflection. The run hands the
+// path back, untouched for the bounce in question, as soon as anything else could
+// happen: the inside cut does not apply, a list sphere is hit first (the run's usual
+// end: the ray leaves through the small glass sphere that overlaps S), the hit is a
+// front face, the reflection is partial (a Schlick draw), or the next bounce would
+// reach the depth cap. Returns the bounces traced (segments).
+__device__ __forceinline__ uint32_t tir_run_64(const SceneView &sv, int S_idx, Path &p, uint32_t max_depth,
+                                               Tally &tl) {
+    const uint32_t lane = __lane_id();
+    const uint32_t info = sv.shd[S_idx].nbr;
+    if (info == rtw_accel::kNbrNone) return 0u;
+    const uint32_t n = info & 0xffu;  // list entries, < 16
+    const uint32_t nl = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(n)));
+    const double4 S = sv.sph[S_idx];
+    const double ratio = sv.shd[S_idx].p;  // back face: ratio = ir (materials.rs:86)
+    // lane j < n: list entry j (inside_hit_group's lane roles); lane n and above: S
+    uint32_t i = static_cast<uint32_t>(S_idx);
+    if (lane < n) {
+        uint32_t e = (info >> 8) + lane;
+        asm volatile("" : "+v"(e));
+        i = sv.nbr[e];
+    }
+    const double4 T = sv.sph[i];
+    const double rrT = T.w * T.w;
+    const uint64_t only_s = 1ull << nl;
+    uint32_t k = 0;
+    while (p.depth + 1u < max_depth) {
+        const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+        // inside_hit_group (kG = 64), the same operations per lane
+        const double ocx = p.ox - T.x, ocy = p.oy - T.y, ocz = p.oz - T.z;
+        const double hb = ocx * p.dx + ocy * p.dy + ocz * p.dz;
+        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - rrT;
+        const double disc = hb * hb - a * c;
+        const double sq = __builtin_sqrt(disc);
+        const double tn = (-sq - hb) / a, tf = (sq - hb) / a;
+        const bool s_ok = (c <= 3. * rrT) && !(hb >= 0. && c >= 0.) && disc >= 0. && !(tn >= 0.01) && tf >= 0.01;
+        const double t = tn >= 0.01 ? tn : tf;
+        const bool cand = lane < n ? (disc >= 0. && t >= 0.01) : lane == n;
+        if (!__builtin_amdgcn_readlane(static_cast<int>(s_ok), nl)) break;  // no inside cut: the scan
+        double bt;
+        if (__ballot(cand) == only_s) {
+            bt = readlane_f64(tf, nl);
+        } else {  // a list sphere has an accepted root too (inside an overlap): the minimum
+            int b = cand ? static_cast<int>(i) : -1;
+            bt = lane == n ? tf : t;
+            dpp_min_step<0xB1>(bt, b);   // quad_perm [1,0,3,2]
+            dpp_min_step<0x4E>(bt, b);   // quad_perm [2,3,0,1]
+            dpp_min_step<0x141>(bt, b);  // row_half_mirror
+            dpp_min_step<0x140>(bt, b);  // row_mirror
+            if (__builtin_amdgcn_readlane(b, 0) != S_idx) break;  // another sphere is hit: the generic loop
+            bt = readlane_f64(bt, 0u);
+        }
+        // shade (dielectric): unit(dir), the hit record, the reflection
+        double vx = p.dx, vy = p.dy, vz = p.dz;
+        rtw_num::div3(vx, vy, vz, __builtin_sqrt(a));
+        const double px = p.dx * bt + p.ox, py = p.dy * bt + p.oy, pz = p.dz * bt + p.oz;
+        double nx = px - S.x, ny = py - S.y, nz = pz - S.z;
+        rtw_num::div3(nx, ny, nz, S.w);
+        if ((p.dx * nx + p.dy * ny + p.dz * nz) < 0.) break;  // a front face: the generic loop
+        nx = -nx, ny = -ny, nz = -nz;
+        const double cos_t = fmin((-vx) * nx + (-vy) * ny + (-vz) * nz, 1.);
+        if (!rtw_num::tir_exceeds(ratio, 1.0 - cos_t * cos_t, 1.)) break;  // Schlick's draw: the generic loop
+        const double dt = vx * nx + vy * ny + vz * nz;
+        p.dx = vx - (nx * dt) * 2., p.dy = vy - (ny * dt) * 2., p.dz = vz - (nz * dt) * 2.;
+        p.ox = px, p.oy = py, p.oz = pz;
+        ++p.depth;  // p.prev stays S
+        ++k;
+        if (lane == 0) tl.inside += 1u, tl.ntest += 1u + n;
+    }
+    return k;
+}
+
 // Phase 2: the parked pixels, kG lanes per pixel. Persistent groups take pixels
 // in park order (the heaviest parked first) from an atomic cursor. Scene::hit is
 // split across the group: lane j filters spheres j, j + kG, ... against the
@@ -1491,7 +1582,12 @@ __device__ __forceinline__ uint32_t coop_pixel(const KParams &P, const SceneView
     // on one path with one RNG state: only 64-lane groups take it
     constexpr bool kWaveReplay = kG == 64;
     static_assert(!kWaveReplay || kG == 64, "the trapped-path replay runs on whole waves only");
-    trace_samples<true, kWaveReplay>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    if constexpr (kWaveReplay) {
+        auto run = [&](Path &p, int S_idx) { return tir_run_64(sv, S_idx, p, P.max_depth, tl); };
+        trace_samples<true, true>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped, run);
+    } else {
+        trace_samples<true, false>(P, sv, q.x, y, KP(spill_b), col, ps, 0xffffffffu, s, stp, hit, &trapped);
+    }
     if (sub == 0) tl.trap += trapped;
     if (sub == 0) {
         write_pixel(P, q.x, q.lr, ps);
@@ -1585,31 +1681,31 @@ __global__ __launch_bounds__(kProbeBlock) void rtw_cost_probe(const KParams P) {
         const uint32_t lr = qr * sub, x = qx * sub;
         const uint64_t i = static_cast<uint64_t>(lr) * P.W + x;
         const uint32_t wgt = min(sub, P.W - x) * min(sub, P.n_rows - lr);
-        const PixelLoc pl(P, x, P.row_begin + lr * P.row_step);
         // the probe's own stream (a hash of the render seed and the global pixel index),
         // not the pixel's RNG child: the estimate is as good, and the probe no longer
         // waits for rtw_seed_pixels, which runs beside it on the session's second stream
-        U128 rng = probe_state(P.seed_lo, P.seed_hi, static_cast<uint64_t>(P.row_begin + lr * P.row_step) * P.W + x);
-        uint32_t segs = 0;
-        for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
-            Path p;
-            gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p, stp);
-            for (;;) {  // one path, at most probe_cap segments (only counted: no attenuation rows kept)
-                ++segs;
-                const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
-                double bt = 0.;
-                const int best = bvh_hit<kLds, kProbeBlock>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
-                if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= P.probe_cap) break;
-                double cr, cg, cb;
-                shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
-                p.stk.clear();  // the register slots never fill, whatever the cap
+        auto probe_pixel = [&](uint32_t px_, uint32_t lr_) {
+            const PixelLoc pl(P, px_, P.row_begin + lr_ * P.row_step);
+            U128 rng = probe_state(P.seed_lo, P.seed_hi, static_cast<uint64_t>(P.row_begin + lr_ * P.row_step) * P.W + px_);
+            uint32_t segs = 0;
+            for (uint32_t q = 0; q < kProbeSamples && P.max_depth > 0; ++q) {
+                Path p;
+                gen_ray(P, pl, (q * P.n_off) / kProbeSamples, rng, p, stp);
+                for (;;) {  // one path, at most probe_cap segments (only counted: no attenuation rows kept)
+                    ++segs;
+                    const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
+                    double bt = 0.;
+                    const int best = bvh_hit<kLds, kProbeBlock>(P, sv, p.ox, p.oy, p.oz, p.dx, p.dy, p.dz, a, p.prev, bt, tl, stp, scol);
+                    if (best < 0 || p.depth + 1 >= P.max_depth || p.depth + 1 >= P.probe_cap) break;
+                    double cr, cg, cb;
+                    shade(P, sv.sph, sv.shd, best, bt, a, p, rng, nullptr, 0, 0, cr, cg, cb, stp);
+                    p.stk.clear();  // the register slots never fill, whatever the cap
+                }
             }
-        }
+            return segs;
+        };
+        const uint32_t segs = probe_pixel(x, lr);
         P.pcost[i] = segs;
-        // the tile's cost word (hot pixels: its hot count), summed over the wave's lanes
-        // that share it before one atomic per word: consecutive lanes hold consecutive
-        // pixels, so a wave touches ~9 tile words -- one device-scope atomic (32 B of HBM
-        // writes) per word instead of one per pixel (25 MB a frame)
         const TileGrid tg(P);
         const bool hot = segs >= P.hot_segs;
         const uint32_t key = (hot ? tg.count() : 0u) + tg.of(x, lr);
