@@ -385,11 +385,7 @@ __global__ __launch_bounds__(kBlock, 2) void rtw_fast_render(const FastParams P)
                 if (lane < 3) {
                     const double v = static_cast<double>(acc[wave][s][lane]) * (1. / 4294967296.) /
                                      static_cast<double>(P.n_off);
-#if RTW_FB_NT  // streaming store (A/B; rtw_render.hip write_pixel)
-                    __builtin_nontemporal_store(static_cast<float>(v), P.out + static_cast<uint64_t>(pixs[s]) * 3u + lane);
-#else
                     P.out[static_cast<uint64_t>(pixs[s]) * 3u + lane] = static_cast<float>(v);
-#endif
                 }
                 pixs[s] = kFree;
                 ++written;

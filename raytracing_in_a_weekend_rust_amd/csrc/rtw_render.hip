@@ -929,9 +929,6 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
     return false;
 }
 
-#ifndef RTW_FB_NT
-#define RTW_FB_NT 0  // framebuffer stores non-temporal (A/B)
-#endif
 // RTW_KARG_SELFTEST (`make karg-selftest` only, never a library): write_pixel outlined,
 // so the karg guard must reject the build
 #ifdef RTW_KARG_SELFTEST
@@ -944,19 +941,9 @@ __device__ RTW_KARG_HELPER void write_pixel(const KParams &P, uint32_t x, uint32
     if (count && KP(pixels_done)) atomicAdd(KP(pixels_done), 1u);
     const double nf = static_cast<double>(KP(n_off));
     double *o = KP(out) + (static_cast<uint64_t>(lr) * KP(W) + x) * 3u;
-#if RTW_FB_NT
-    // streaming stores: a pixel's 24 B are its last write to those bytes in the
-    // launch, and its neighbours complete at other times (cost-ordered hand-out), so
-    // a line kept dirty in L2 is written back part by part (2.08x the framebuffer's
-    // bytes, profiles/r03_misc)
-    __builtin_nontemporal_store(ps.ar / nf, o);
-    __builtin_nontemporal_store(ps.ag / nf, o + 1);
-    __builtin_nontemporal_store(ps.ab / nf, o + 2);
-#else
     o[0] = ps.ar / nf;
     o[1] = ps.ag / nf;
     o[2] = ps.ab / nf;
-#endif
 }
 
 // Exact f64 Sphere::hit (sphere.rs:39-71) of sphere i against the current best,
