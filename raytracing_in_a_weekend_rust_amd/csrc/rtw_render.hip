@@ -161,6 +161,8 @@ struct KParams {
     uint32_t drain_prio;        // draining waves' issue priority after the cursor phase (RTW_DRAIN_PRIO,
                                 // default 3; 0: unchanged)
     uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
+    uint32_t prio_split;        // > 0 (RTW_PRIO_SPLIT, segments per sample x 8): a drained pixel below
+                                // it drains at priority 0, the others at the drain priority
     uint32_t spread_q;          // > 0: hand-out ticket t < 64 q takes order position (t % 64) q + t / 64,
                                 // so a wave's 64 lanes get pixels from across the cost order
                                 // (RTW_SPREAD; 0: position t)
@@ -1917,6 +1919,9 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
             for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // per-pixel issue priority (RTW_PRIO_SPLIT): the long chains at the waves'
+            // priority, the others at the cursor waves' (0)
+            if (P.prio_split) set_prio(q._pad >= P.prio_split ? KP(heavy_prio) : 0u);
             cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid() & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
             if (sub == 0) atomicAdd(P.park_processed, 1u);
         }
@@ -1979,7 +1984,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         // from its first sample
                         diag_event(P, npix, pix, 1);
                         Parked q;
-                        q.x = x, q.lr = lr, q.k = 0, q._pad = 0;
+                        q.x = x, q.lr = lr, q.k = 0, q._pad = KP(pcost)[pix] * 4u;  // 8 x segments per sample (2 probe samples)
                         q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
                         q.ar = q.ag = q.ab = 0., q._pad2 = 0.;
                         publish_parked(P, q);
@@ -2237,7 +2242,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     diag_event(P, npix, pix, 1);
                     ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
                     Parked q;
-                    q.x = x, q.lr = lr, q.k = ps.k, q._pad = 0;
+                    q.x = x, q.lr = lr, q.k = ps.k, q._pad = (pseg * 8u) / max(ps.k, 1u);  // 8 x segments per sample so far
                     q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
                     q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
                     publish_parked(P, q);
@@ -2327,6 +2332,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         gu64 *src = (gu64 *)(P.park + t);
 #pragma unroll
         for (int j = 0; j < 8; ++j) w[j] = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (P.prio_split) set_prio(q._pad >= P.prio_split ? KP(drain_prio) : 0u);
         cseg += coop_pixel<kCoopG>(P, sv, filt, fsh, q, gid() & ~static_cast<uint64_t>(kCoopG - 1u), tl, stp_unused);
         if (sub == 0) atomicAdd(P.park_processed, 1u);
     }
@@ -3058,6 +3064,8 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
         if (const char *e = kn.get("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (const char *e = kn.get("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
+        P.prio_split = 0;
+        if (const char *e = kn.get("RTW_PRIO_SPLIT")) P.prio_split = static_cast<uint32_t>(std::max(0., std::atof(e) * 8.));
         P.spread_q = 0;
         if (const char *e = kn.get("RTW_SPREAD"))
             if (std::atoi(e) != 0 && P.order_map) P.spread_q = static_cast<uint32_t>(npix / 64u);
