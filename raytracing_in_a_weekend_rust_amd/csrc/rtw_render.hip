@@ -79,6 +79,8 @@ constexpr uint32_t kSmallShardPrepark = 16; // small shards: probe segments (2 s
                                             // pixel before its first sample
 constexpr double kJoinPct = 35.;        // ... which join the cursor after this % of the pixels
 constexpr uint32_t kEndgameMinSamples = 4;  // endgame parking: only pixels with this many samples left
+constexpr uint32_t kPrioSplit8 = 20u * 8u;  // drains of pixels above 20 segments/sample keep the raised
+                                            // priority (x 8: Parked::_pad's fixed point)
 #ifndef RTW_ENDGAME_POLL
 #define RTW_ENDGAME_POLL 16
 #endif
@@ -3064,7 +3066,13 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         P.drain_prio = 3, P.heavy_prio = small_fill ? 3u : 0u;
         if (const char *e = kn.get("RTW_HEAVY_PRIO")) P.heavy_prio = static_cast<uint32_t>(std::min(3, std::max(0, std::atoi(e))));
         if (const char *e = kn.get("RTW_PREPARK")) P.prepark = static_cast<uint32_t>(std::atoi(e));
-        P.prio_split = 0;
+        // per-pixel drain priority in a shard of about one pixel per lane (N=4 of the
+        // bench image, half the waves drain): only pixels estimated at >= 20 segments per
+        // sample (the long serial chains) drain at the raised priority, the others at
+        // the cursor waves' -- rank 60.2 -> 56.8 ms (mean of 3 maxima); at N=8 (fewer
+        // pixels than lanes) it loses, 48.0 -> 49.4 ms, so it is off there
+        // (profiles/r06_misc/knobs_prio_split.log, strong_repeats_prio_split.log)
+        P.prio_split = fill >= 0.75 && small_fill ? kPrioSplit8 : 0u;
         if (const char *e = kn.get("RTW_PRIO_SPLIT")) P.prio_split = static_cast<uint32_t>(std::max(0., std::atof(e) * 8.));
         P.spread_q = 0;
         if (const char *e = kn.get("RTW_SPREAD"))
