@@ -165,6 +165,7 @@ struct KParams {
     uint32_t heavy_prio;        // priority waves' issue priority while they drain (RTW_HEAVY_PRIO, default 3)
     uint32_t prio_split;        // > 0 (RTW_PRIO_SPLIT, segments per sample x 8): a drained pixel below
                                 // it drains at priority 0, the others at the drain priority
+    uint32_t wave_cap;          // > 0 (RTW_WAVE_CAP, A/B): a cursor wave holds at most wave_cap pixels
     uint32_t spread_q;          // > 0: hand-out ticket t < 64 q takes order position (t % 64) q + t / 64,
                                 // so a wave's 64 lanes get pixels from across the cost order
                                 // (RTW_SPREAD; 0: position t)
@@ -428,8 +429,24 @@ __host__ __device__ inline size_t lds_bytes_for(uint32_t n, uint32_t n_node, uin
 // Persistent kernel, per-lane LDS areas after the scene view: the running pixel
 // sum (3 x f64 columns), the BVH walk scratch (kScratch x u16 columns) and the
 // speculative draws' RNG state (one 16 B column).
-__host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
+__host__ __device__ constexpr size_t lane_lds_area(uint32_t threads) {
     return static_cast<size_t>(threads) * (3 * sizeof(double) + rtw_accel::kScratch * sizeof(uint16_t) + 16);
+}
+// + one u32 per workgroup after the lanes' areas: its cursor waves' completions,
+// posted to pixels_done as each cursor wave leaves its loop (RTW_WG_DONE=0 builds: one
+// device-scope atomic on pixels_done per wave iteration with a completion, as before
+// round 6). Those atomics all hit one word from every CU; a wave's later
+// s_waitcnt vmcnt(0) waits for its own, so at 100 spp -- five times the completions
+// per segment of the headline -- they held the waves: config 3 26.62 -> 24.23 ms,
+// the headline 119.19 -> 118.97 ms, the persistent kernel's writes 166 -> 140 MB
+// (profiles/r06_misc/ab_wg_done.log). Launches with the endgame, whose trigger reads
+// the count, keep the global atomic.
+#ifndef RTW_WG_DONE
+#define RTW_WG_DONE 1
+#endif
+constexpr bool kWgDone = RTW_WG_DONE != 0;
+__host__ __device__ constexpr size_t lane_lds_bytes(uint32_t threads) {
+    return lane_lds_area(threads) + 16u;
 }
 // One camera path in flight (the ray_color recursion flattened): the current
 // ray, its depth and the material rows of its non-dielectric bounces.
@@ -1825,7 +1842,10 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
 template <bool kLds, int kMode, uint32_t kThreads, uint32_t kCoopG = 16>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
+    if (kWgDone && threadIdx.x == 0)
+        *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_sph) + P.lane_lds_off + lane_lds_area(kThreads)) = 0u;
     const SceneView sv = stage_scene<kLds, kMode>(P, lds_sph);
+    if (kWgDone && !kLds) __syncthreads();  // (kLds: stage_scene's barrier orders the zero)
     // pass-1 records after the scene view: after the inside-cut lists (BVH) or the
     // shading records
     // BVH scenes in LDS: the leaves (indexed by sphere, every sphere's record, rtw_accel.h)
@@ -1948,14 +1968,20 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             if (need && !dry) {  // refill: one atomic for the wave's idle lanes
                 const uint64_t m = __ballot(1);
                 const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
-                uint32_t base = 0;
-                if (rank == 0) base = atomicAdd(KP(pix_cursor), static_cast<uint32_t>(__popcll(m)));
+                uint32_t base = 0, take = static_cast<uint32_t>(__popcll(m));
+                if (const uint32_t cap = KP(wave_cap)) {  // RTW_WAVE_CAP (A/B): at most cap pixels per wave
+                    const uint32_t live = 64u - take;
+                    take = cap > live ? min(take, cap - live) : 0u;
+                }
+                if (rank == 0 && take) base = atomicAdd(KP(pix_cursor), take);
 #ifdef RTW_WALK_DIAG  // diagnostic build: device-scope atomics of the cursor loop
                 if (rank == 0) atomicAdd(&P.counters[16], 1ull);
 #endif
                 base = __shfl(base, __ffsll(static_cast<unsigned long long>(m)) - 1);
                 const uint64_t ticket = static_cast<uint64_t>(base) + rank;
-                if (ticket < npix) {
+                if (rank >= take) {
+                    // over the wave's cap (RTW_WAVE_CAP): stays idle
+                } else if (ticket < npix) {
                     // hand-out order: by descending estimated cost (P.order_map,
                     // rtw_cost_probe), so the cheapest pixels fill the drain; else
                     // rows bottom-up when P.order == 1, or row-major
@@ -2012,7 +2038,15 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 endgame = static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(ld_rlx(KP(pixels_done)))) + P.endgame >= npix;
 
             if (__all(need)) {
-                if (dry) break;
+                if (dry) {
+                    if (kWgDone && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(__ballot(1))) - 1)) {
+                        uint32_t *wg = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_sph) + KP(lane_lds_off) +
+                                                                    lane_lds_area(kThreads));
+                        const uint32_t c = atomicExch(wg, 0u);
+                        if (c) atomicAdd(KP(pixels_done), c);
+                    }
+                    break;
+                }
                 continue;
             }
             if (need) continue;  // this lane waits while the others work
@@ -2141,8 +2175,16 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 }
                 {  // one completion-count atomic per wave (write_pixel leaves it to us)
                     const uint64_t dm = __ballot(done);
-                    if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
-                        atomicAdd(KP(pixels_done), static_cast<uint32_t>(__popcll(dm)));
+                    if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1)) {
+                        // RTW_WG_DONE: an LDS add without the endgame (whose trigger reads the
+                        // global count); the workgroup's sum is posted as its cursor waves leave
+                        if (kWgDone && !KP(endgame))
+                            atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_sph) + KP(lane_lds_off) +
+                                                                   lane_lds_area(kThreads)),
+                                      static_cast<uint32_t>(__popcll(dm)));
+                        else
+                            atomicAdd(KP(pixels_done), static_cast<uint32_t>(__popcll(dm)));
+                    }
 #ifdef RTW_WALK_DIAG
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1))
                         atomicAdd(&P.counters[17], 1ull);
@@ -3073,6 +3115,15 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // pixels than lanes) it loses, 48.0 -> 49.4 ms, so it is off there
         // (profiles/r06_misc/knobs_prio_split.log, strong_repeats_prio_split.log)
         P.prio_split = fill >= 0.75 && small_fill ? kPrioSplit8 : 0u;
+        // shards with fewer pixels than cursor lanes (N=8 of the bench image): the first
+        // fill spreads them over every cursor wave (~40 per wave) instead of filling the
+        // first waves and leaving the rest idle (profiles/r06_misc/ab_refill_chunk_wave_cap.log,
+        // strong_repeats_wave_cap.log)
+        {
+            const uint64_t cw = static_cast<uint64_t>(grid_p) * (wpb - heavy);
+            P.wave_cap = fill < 0.75 && cw ? static_cast<uint32_t>(std::min<uint64_t>(64u, (npix + cw - 1) / cw)) : 0u;
+        }
+        if (const char *e = kn.get("RTW_WAVE_CAP")) P.wave_cap = static_cast<uint32_t>(std::min(64, std::max(0, std::atoi(e))));
         if (const char *e = kn.get("RTW_PRIO_SPLIT")) P.prio_split = static_cast<uint32_t>(std::max(0., std::atof(e) * 8.));
         P.spread_q = 0;
         if (const char *e = kn.get("RTW_SPREAD"))
