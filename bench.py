@@ -62,7 +62,7 @@ HBM_PEAK = 8000.0         # GB/s (MI355X_MICROARCH.md)
 GPU_CLOCK_HZ = 2.4e9      # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMD_LANES = 32           # a SIMD issues 32 lanes per cycle: a wave64 f32/int op takes 2 cycles
 MAIN_KERNEL = {"parity": "rtw_render_persist", "fast": "rtw_fast_render"}
-PMC_FALLBACK = os.path.join(HERE, "profiles", "r05_pmc.json")  # stamped with the build id
+PMC_FALLBACK = os.path.join(HERE, "profiles", "r06_pmc.json")  # stamped with the build id
 # counter passes (never combined with tracing; FETCH_SIZE and WRITE_SIZE never share
 # a pass: MI355X_MICROARCH.md, rocprofv3 block limits)
 PMC_PASSES = {
@@ -98,7 +98,7 @@ def parse():
                    help="0 disables the end-to-end leg (one-shot ABI call with host buffers + PPM)")
     p.add_argument("--pmc", type=int, default=1,
                    help="1: rocprofv3 --pmc passes of a one-frame child run (N=1, after the timed "
-                        "region); 0: only the build-stamped profiles/r05_pmc.json")
+                        "region); 0: only the build-stamped profiles/r06_pmc.json")
     p.add_argument("--cpu-row-stride", type=int, default=0,
                    help="oracle renders every k-th row (0 = auto, ~10-30 s)")
     p.add_argument("--pmc-out", default="",
@@ -223,12 +223,12 @@ def pmc_fallback(kernel, build_id):
         with open(PMC_FALLBACK) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, "no profiles/r05_pmc.json"
+        return None, "no profiles/r06_pmc.json"
     if d.get("kernel") != kernel or d.get("workload") != "complex_1200x675_s23_d50":
-        return None, "profiles/r05_pmc.json is for another kernel/workload"
+        return None, "profiles/r06_pmc.json is for another kernel/workload"
     if d.get("build_id") != build_id:
-        return None, f"profiles/r05_pmc.json is from build {d.get('build_id')}, library is {build_id}: refused"
-    return d, "profiles/r05_pmc.json (same build id)"
+        return None, f"profiles/r06_pmc.json is from build {d.get('build_id')}, library is {build_id}: refused"
+    return d, "profiles/r06_pmc.json (same build id)"
 
 
 # ------------------------------------------------------------ other legs --
