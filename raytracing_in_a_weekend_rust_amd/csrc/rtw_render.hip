@@ -714,11 +714,7 @@ __device__ __forceinline__ uint64_t unit_vec_round(const uint4 *__restrict__ tri
             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(s.hi >> 32))))
         __builtin_trap();
 #endif
-    // the column offset formed per call from a laundered lane id: hoisted, the compiler
-    // held it as a 64-bit value through the drain loop and spilled it to scratch
-    uint32_t lcol = lane;
-    asm volatile("" : "+v"(lcol));
-    const uint4 *col = tries + lcol;
+    const uint4 *col = tries + lane;
     uint64_t lo = 0, hi = 0;
     for (uint32_t h = 0; h < 2; ++h) {
         uint64_t m = h ? s.hi : s.lo;
@@ -903,19 +899,11 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
         return false;
     }
     if (ps.k >= n_off) return false;
-    // the pixel's position formed per sample from a laundered x: held from here to the
-    // pixel's end, the compiler spilled it to scratch (a reload per sample)
-    auto pl = [&]() {
-        uint32_t xx = x;
-#ifndef RTW_AB_PL_HOLD
-        asm volatile("" : "+v"(xx));
-#endif
-        return PixelLoc(P, xx, y);
-    };
+    const PixelLoc pl(P, x, y);
     const uint64_t stride = P.spill_stride;
     Path p;
     int tir_no = -1;  // kTrap: S whose great-circle test failed on the last TIR bounce
-    gen_ray(P, pl(), ps.k, ps.rng, p, stp);
+    gen_ray(P, pl, ps.k, ps.rng, p, stp);
     STAMP(0);  // 0: seed jump + pixel setup
     for (;;) {
         // ---- Scene::hit (hittable.rs:131-143): first minimum over all spheres ----
@@ -955,7 +943,7 @@ __device__ __forceinline__ bool trace_samples(const KParams &P, const SceneView 
             else fold(sv.shd, p, spill, col, stride, lr, lg, lb, ps);
             if (++ps.k >= n_off) break;
             if (seg >= budget) return true;  // sample boundary: hand the rest to the coop kernel
-            gen_ray(P, pl(), ps.k, ps.rng, p, stp);
+            gen_ray(P, pl, ps.k, ps.rng, p, stp);
         }
         STAMP(4);  // 4: fold + next sample
     }
@@ -1070,86 +1058,11 @@ __device__ __forceinline__ int scan_hit(const KParams &P, const double4 *__restr
     return best;
 }
 
-// ---- Two-lane walk split (RTW_PAIR) --------------------------
-// In shards with fewer pixels than lanes a pixel may take two adjacent lanes (2j,
-// 2j + 1) of a cursor wave. Both lanes hold the same path, draw the same numbers and
-// run the same scatter (one lane's worth of instructions: the wave issues them once);
-// the walk is what they split. Lane `sub` loads the half plane rows of children
-// 2 sub and 2 sub + 1 (ds_read_b64 instead of b128), runs their two slab tests, and
-// the pair exchanges its hit bits by DPP (quad_perm [1,0,3,2]); each lane filters the
-// leaf children of its own slots into its own candidate list, and after the node the
-// pair takes the smaller cut U -- so both lanes visit exactly the nodes the one-lane
-// walk visits (the slab tests use the U every earlier leaf left; leaf_test's keep
-// decision does not read U), and the two candidate lists partition the one-lane
-// walk's. Overflow (`bad`) is OR-ed over the pair, so the lanes leave together. The
-// exact tests then run on each lane's own list and the pair's (t, index) minimum is
-// the scan's first minimum (rtw_accel::better), hittable.rs:131-143.
-__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xf, 0xf, false));
-}
-__device__ __forceinline__ void pair_min(double &bt, int &best) {
-    const int ob = __builtin_amdgcn_update_dpp(-1, best, 0xB1, 0xf, 0xf, false);
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(bt), 0xB1, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(bt), 0xB1, 0xf, 0xf, false);
-    const double ot = __hiloint2double(hi, lo);
-    const bool take = (ob >= 0) & ((best < 0) | (ot < bt) | ((ot == bt) & (ob < best)));  // rtw_accel::better
-    bt = take ? ot : bt;
-    best = take ? ob : best;
-}
-__device__ __forceinline__ bool walk_pair(const float4 *__restrict__ nodes, const float4 *__restrict__ leaves,
-                                          const rtw_accel::WalkRay &r, float &U, uint32_t &visits,
-                                          rtw_accel::LdsScratch &stk, uint32_t sub) {
-    using rtw_accel::as_f32;
-    using rtw_accel::as_u32;
-    const uint32_t sx = r.neg & 1u, sy = (r.neg >> 1) & 1u, sz = r.neg >> 2;
-    const uint32_t oct_shift = 8u * (r.neg & 3u);
-    const bool oct_hi = r.neg >= 4u;
-    const uint32_t half = 8u * sub;             // byte offset of this lane's children in a plane row
-    const uint32_t own = 3u << (2u * sub);      // this lane's child slots
-    uint32_t cur = 0;
-    for (;;) {
-        ++visits;
-        const char *Nb = reinterpret_cast<const char *>(nodes) + __umul24(cur, 144u);
-        auto row = [&](uint32_t k) { return *reinterpret_cast<const float2 *>(Nb + 16u * k + half); };
-        const float2 nX = row(sx), fX = row(sx ^ 1u), nY = row(2u + sy), fY = row(3u - sy), nZ = row(4u + sz),
-                     fZ = row(5u - sz);
-        const float4 qc = reinterpret_cast<const float4 *>(Nb)[6], qo = reinterpret_cast<const float4 *>(Nb)[7];
-        uint32_t h = (rtw_accel::slab_hit(nX.x, nY.x, nZ.x, fX.x, fY.x, fZ.x, r, U) ? 1u : 0u) |
-                     (rtw_accel::slab_hit(nX.y, nY.y, nZ.y, fX.y, fY.y, fZ.y, r, U) ? 2u : 0u);
-        h <<= 2u * sub;
-        const uint32_t r01 = as_u32(qc.x), r23 = as_u32(qc.y), masks = as_u32(qc.z);
-        const uint32_t hit = (h | pair_swap(h)) & masks;
-        const uint32_t lall = hit & (masks >> 4);
-        const uint32_t inner = hit & ~lall & 15u;
-        const uint64_t refs = (static_cast<uint64_t>(r23) << 32) | r01;
-        uint32_t lmask = lall & own;
-        while (lmask) {
-            const uint32_t j = static_cast<uint32_t>(__builtin_ctz(lmask));
-            lmask &= lmask - 1u;
-            rtw_accel::leaf_test(leaves, static_cast<uint32_t>(refs >> (16u * j)) & 0xffffu, r, U, stk);
-        }
-        U = fminf(U, as_f32(pair_swap(as_u32(U))));
-        const uint32_t ord = ((oct_hi ? as_u32(qo.y) : as_u32(qo.x)) >> oct_shift) & 0xffu;
-        for (int t = 3; t >= 0; --t) {
-            const uint32_t j = (ord >> (2 * t)) & 3u;
-            stk.put(static_cast<uint32_t>(refs >> (16u * j)), __builtin_amdgcn_ubfe(inner, j, 1u));
-        }
-        uint32_t b = stk.bad | (stk.top > stk.lim ? 1u : 0u);
-        b |= pair_swap(b);
-        stk.bad = b;
-        if (b != 0u || stk.top == stk.base) break;
-        stk.top -= stk.stride;
-        cur = *stk.top;
-    }
-    return stk.bad == 0u;
-}
-
 // Scene::hit by the BVH (rtw_accel.h): always-spheres exactly, the f32 walk,
 // exact candidates, the cut check; anything unproven falls back to the scan.
 // kStride: the LDS scratch column stride (the workgroup size; a constant, so the
-// walk's pointer steps are immediates and hold no register). kPair: the two-lane
-// walk split above (kLdsStack only).
-template <bool kLdsStack = false, uint32_t kStride = 0, bool kPair = false>
+// walk's pointer steps are immediates and hold no register)
+template <bool kLdsStack = false, uint32_t kStride = 0>
 __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, double ox, double oy,
                                        double oz, double dx, double dy, double dz, double a, int prev,
                                        double &bt, Tally &tl, Stamps &stp, uint16_t *scol = nullptr,
@@ -1186,22 +1099,15 @@ __device__ __forceinline__ int bvh_hit(const KParams &P, const SceneView &sv, do
                 // after it: every wave that walks with kLdsStack is a cursor wave at that
                 // point (a priority wave that joins the cursor runs as one).
                 if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(kWalkPrio);
-                bool walked;
-                if constexpr (kPair) {
-                    static_assert(!kPair || kLdsStack, "the pair walk runs on the LDS scratch");
-                    walked = walk_pair(nodes, leaves, wr, U, tl.visits, ws, threadIdx.x & 1u);
-                } else {
-                    walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
-                }
+                const bool walked = rtw_accel::walk(nodes, leaves, wr, U, tl.visits, ws);
                 if constexpr (kLdsStack && kWalkPrio > 0) __builtin_amdgcn_s_setprio(0);
                 STAMP(2);  // 2: BVH walk
-                if (!walked) return false;  // pair-uniform with kPair
+                if (!walked) return false;
                 for (uint32_t j = 0; j < ws.nc; ++j) {
                     ++tl.ntest;
                     exact_test(sph, ws.cand_at(j), ox, oy, oz, dx, dy, dz,
                                a, best, bt);
                 }
-                if constexpr (kPair) pair_min(bt, best);
                 return true;
             };
             bool walked;
@@ -1933,9 +1839,8 @@ __global__ __launch_bounds__(kBlock) void rtw_cost_scatter(const KParams P) {
 // cursor ran dry. Groups claim queue tickets in order and wait for a claimed
 // ticket to be published; they stop once every cursor wave has signalled that it
 // parks no more and their ticket lies past the final queue length.
-template <bool kLds, int kMode, uint32_t kThreads, uint32_t kCoopG = 16, bool kPair = false>
+template <bool kLds, int kMode, uint32_t kThreads, uint32_t kCoopG = 16>
 __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) {
-    static_assert(!kPair || (kLds && kMode == kBvh), "the two-lane walk split needs the LDS BVH");
     extern __shared__ __attribute__((aligned(16))) double4 lds_sph[];
     if (kWgDone && threadIdx.x == 0)
         *reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(lds_sph) + P.lane_lds_off + lane_lds_area(kThreads)) = 0u;
@@ -1976,8 +1881,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
     auto hit = [&](double ox, double oy, double oz, double dx, double dy, double dz, double a, int prev,
                    double &bt) -> int {
         if constexpr (kMode == kBvh) {
-            return bvh_hit<true, kThreads, kPair>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp,
-                                                  lane_stk + threadIdx.x, &seg_sa);
+            return bvh_hit<true, kThreads>(P, sv, ox, oy, oz, dx, dy, dz, a, prev, bt, tl, stp,
+                                           lane_stk + threadIdx.x, &seg_sa);
         } else {
             const Seg32 g(ox, oy, oz, dx, dy, dz, a, kMode == kScanF32);
             return scan_hit(P, sph, g, ox, oy, oz, dx, dy, dz, a, bt, tl);
@@ -2045,10 +1950,6 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
         tl.seg += cseg;
     }
     if (cursor_wave) {
-        // kPair: lanes 2j and 2j + 1 hold one pixel (walk_pair); the even lane alone
-        // counts, publishes and writes it
-        const bool lead = !kPair || (lane & 1u) == 0u;
-        constexpr uint64_t kLeadMask = kPair ? 0x5555555555555555ull : ~0ull;
         bool need = true;  // lane holds no pixel
         bool dry = false;  // wave-uniform: the cursor ran dry
         bool endgame = false;  // wave-uniform: latched endgame (P.endgame)
@@ -2066,14 +1967,13 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             bool dry_now = false;
             if (need && !dry) {  // refill: one atomic for the wave's idle lanes
                 const uint64_t m = __ballot(1);
-                const uint64_t lm = m & kLeadMask;  // one bit per idle pixel slot
-                const uint32_t rank = static_cast<uint32_t>(__popcll(lm & ((1ull << (kPair ? lane & ~1u : lane)) - 1ull)));
-                uint32_t base = 0, take = static_cast<uint32_t>(__popcll(lm));
+                const uint32_t rank = static_cast<uint32_t>(__popcll(m & ((1ull << lane) - 1ull)));
+                uint32_t base = 0, take = static_cast<uint32_t>(__popcll(m));
                 if (const uint32_t cap = KP(wave_cap)) {  // RTW_WAVE_CAP (A/B): at most cap pixels per wave
-                    const uint32_t live = (kPair ? 32u : 64u) - take;
+                    const uint32_t live = 64u - take;
                     take = cap > live ? min(take, cap - live) : 0u;
                 }
-                if (rank == 0 && lead && take) base = atomicAdd(KP(pix_cursor), take);
+                if (rank == 0 && take) base = atomicAdd(KP(pix_cursor), take);
 #ifdef RTW_WALK_DIAG  // diagnostic build: device-scope atomics of the cursor loop
                 if (rank == 0) atomicAdd(&P.counters[16], 1ull);
 #endif
@@ -2106,7 +2006,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     spec = false;
                     if (KP(max_depth) == 0) {  // every sample black, no Scene::hit call
                         ps.k = KP(n_off);
-                        if (lead) write_pixel(P, x, lr, ps);
+                        write_pixel(P, x, lr, ps);
                     } else if (P.prepark && order_map && KP(pcost)[pix] >= P.prepark) {
                         // a long serial chain by the probe's estimate: to a drain wave
                         // from its first sample
@@ -2115,8 +2015,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                         q.x = x, q.lr = lr, q.k = 0, q._pad = KP(pcost)[pix] * 4u;  // 8 x segments per sample (2 probe samples)
                         q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
                         q.ar = q.ag = q.ab = 0., q._pad2 = 0.;
-                        if (lead) publish_parked(P, q);
-                        tl.parked += lead ? 1u : 0u;
+                        publish_parked(P, q);
+                        ++tl.parked;
                     } else {
                         gen_ray(P, PixelLoc(P, x, KP(row_begin) + lr * KP(row_step)), 0, ps.rng, p, stp);
                         need = false;
@@ -2150,7 +2050,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                 continue;
             }
             if (need) continue;  // this lane waits while the others work
-            tl.seg += lead ? 1u : 0u, ++pseg;
+            ++tl.seg, ++pseg;
             const double a = p.dx * p.dx + p.dy * p.dy + p.dz * p.dz;
             double bt = 0.;
             STAMP(0);  // 0: loop top, refill
@@ -2267,14 +2167,14 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                                  (endgame && KP(n_off) - ps.k >= kEndgameMinSamples) ||
                                  (dry && static_cast<uint64_t>(KP(n_off) - ps.k) * pseg > static_cast<uint64_t>(KP(tail_segs)) * ps.k));
                 uint32_t *diag = KP(diag);
-                if ((done || park) && diag && lead) {  // a pixel's records may come from two XCDs
+                if ((done || park) && diag) {  // a pixel's records may come from two XCDs
                     atomicAdd(diag + 2 * pix, pseg);
                     __hip_atomic_store((gu32 *)(diag + 2 * pix + 1),
                                        static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime()),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 {  // one completion-count atomic per wave (write_pixel leaves it to us)
-                    const uint64_t dm = __ballot(done) & kLeadMask;
+                    const uint64_t dm = __ballot(done);
                     if (dm && lane == static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(dm)) - 1)) {
                         // RTW_WG_DONE: an LDS add without the endgame (whose trigger reads the
                         // global count); the workgroup's sum is posted as its cursor waves leave
@@ -2380,7 +2280,7 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
             if (ended) {
                 if (done) {
                     ps.ar = acc[0], ps.ag = acc[kThreads], ps.ab = acc[2 * kThreads];
-                    if (lead) write_pixel(P, x, lr, ps, false);
+                    write_pixel(P, x, lr, ps, false);
                     need = true;
                 } else if (park) {  // park at the sample boundary
                     diag_event(P, npix, pix, 1);
@@ -2389,8 +2289,8 @@ __global__ __launch_bounds__(kThreads) void rtw_render_persist(const KParams P) 
                     q.x = x, q.lr = lr, q.k = ps.k, q._pad = (pseg * 8u) / max(ps.k, 1u);  // 8 x segments per sample so far
                     q.rng_lo = ps.rng.lo, q.rng_hi = ps.rng.hi;
                     q.ar = ps.ar, q.ag = ps.ag, q.ab = ps.ab, q._pad2 = 0.;
-                    if (lead) publish_parked(P, q);
-                    tl.parked += lead ? 1u : 0u;
+                    publish_parked(P, q);
+                    ++tl.parked;
                     need = true;
                 } else {  // the next sample's defocus disk point (camera.rs:452-456)
                     const double dpx = -1. + 2. * rtw_num::next01_of(dm0), dpy = -1. + 2. * rtw_num::next01_of(dm1);
@@ -3153,22 +3053,6 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // knobs_heavy_rate_endgame.log)
         const double fill = static_cast<double>(npix) / (static_cast<double>(grid_p) * pblock);
         const bool small_fill = fill < 1.5;  // strong scaling at N >= 4 of the bench image
-        // two-lane walk split (walk_pair; RTW_PAIR=1: shards of fewer pixels than 3/4 of the
-        // launch's lanes, 2: any shard) -- A/B only
-        bool pair = false;
-        if (const char *e = kn.get("RTW_PAIR")) {
-            const int v = std::atoi(e);
-            pair = fn == reinterpret_cast<const void *>(&rtw_render_persist<true, kBvh, kPBlock, 64>) &&
-                   (v == 2 || (v == 1 && fill < 0.75));
-        }
-        if (pair) {
-            const void *fp = reinterpret_cast<const void *>(&rtw_render_persist<true, kBvh, kPBlock, 64, true>);
-            int pcu = 0;
-            HIPCHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pcu, fp, pblock, lds));
-            if (pcu == per_cu) fn = fp;
-            else pair = false;
-        }
-        if (kn.get("RTW_PAIR")) std::fprintf(stderr, "[rtw] RTW_PAIR: two-lane walk split %s (fill %.3f)\n", pair ? "on" : "off", fill);
         // (fewer samples per pixel, shorter chains, fewer drains wanted: 4 at 100 spp,
         // rank 23.0 -> 17.9 ms at s=10 with the rate rule's earlier start below)
         uint32_t heavy = fill >= 0.75 && small_fill ? (P.n_off >= 400u ? kHeavyPerBlockFull : kHeavyPerBlockFullShort)
@@ -3237,7 +3121,7 @@ void render(rtw_session *s, const rtw_camera *cam, uint32_t samples_sqrt, rtw_u1
         // strong_repeats_wave_cap.log)
         {
             const uint64_t cw = static_cast<uint64_t>(grid_p) * (wpb - heavy);
-            P.wave_cap = fill < 0.75 && cw ? static_cast<uint32_t>(std::min<uint64_t>(pair ? 32u : 64u, (npix + cw - 1) / cw)) : 0u;
+            P.wave_cap = fill < 0.75 && cw ? static_cast<uint32_t>(std::min<uint64_t>(64u, (npix + cw - 1) / cw)) : 0u;
         }
         if (const char *e = kn.get("RTW_WAVE_CAP")) P.wave_cap = static_cast<uint32_t>(std::min(64, std::max(0, std::atoi(e))));
         if (const char *e = kn.get("RTW_PRIO_SPLIT")) P.prio_split = static_cast<uint32_t>(std::max(0., std::atof(e) * 8.));
